@@ -1,0 +1,114 @@
+"""ctypes binding of libcosnet_hip.so (the C ABI declared in include/cosnet_hip.h).
+
+The library is the only compute path: if it is missing or cannot be loaded on a GPU box,
+every op raises instead of falling back to anything else.  torch must be imported before
+the library is loaded so that both share torch's HIP runtime (same soname).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libcosnet_hip.so")
+
+DT_F32 = 0
+DT_BF16 = 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_longlong
+_F = ctypes.c_float
+_S = ctypes.c_size_t
+
+# name -> (restype, argtypes); stream is always the last argument (void*)
+_SIGS = {
+    "cn_conv_fwd": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I, _P]),
+    "cn_conv_dgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _L, _I, _I, _I, _P]),
+    "cn_conv_wgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "cn_gemm": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _I, _I, _F, _P, _I, _I, _P]),
+    "cn_bn_workspace_floats": (_S, [_I, _I, _I]),
+    "cn_bn_stats": (_I, [_I, _P, _L, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P]),
+    "cn_bn_eval_params": (_I, [_P, _P, _I, _F, _P, _P, _P]),
+    "cn_bn_apply": (_I, [_I, _P, _L, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P, _P, _L, _P]),
+    "cn_bn_bwd": (_I, [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P]),
+    "cn_coatt_workspace_floats": (_S, [_I, _I, _I]),
+    "cn_coatt_softmax": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "cn_coatt_dscore": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "cn_nchw_to_nhwc": (_I, [_I, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "cn_weight_prep": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "cn_maxpool_fwd": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "cn_maxpool_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "cn_avgpool": (_I, [_I, _P, _L, _I, _I, _I, _F, _P, _P]),
+    "cn_bcast_rows": (_I, [_I, _P, _I, _I, _I, _F, _P, _L, _I, _P]),
+    "cn_gate_fwd": (_I, [_I, _P, _L, _I, _I, _P, _P, _P, _L, _P, _P]),
+    "cn_gate_bwd": (_I, [_I, _P, _L, _P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _P, _P]),
+    "cn_head_fwd": (_I, [_I, _P, _L, _P, _L, _I, _I, _I, _P, _P, _P, _L, _P, _P]),
+    "cn_head_bwd": (_I, [_I, _P, _L, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P]),
+    "cn_upsample_sigmoid": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "cn_upsample_sigmoid_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "cn_count_ge": (_I, [_P, _L, _F, _P, _P]),
+    "cn_loss_workspace_floats": (_S, [_L]),
+    "cn_bce_l1": (_I, [_P, _P, _L, _F, _F, _P, _P, _P, _P]),
+    "cn_sgd": (_I, [_P, _I, _P, _F, _F, _P]),
+    "cn_rowdot": (_I, [_I, _P, _L, _P, _L, _I, _I, _P, _P]),
+    "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P]),
+    "cn_cast2d": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _I, _P]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the library (once).  Raises NativeError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError("libcosnet_hip.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return sorted(_SIGS.keys())
+
+
+_ERR = {-1: "shape", -2: "alignment", -3: "unsupported", -4: "hip runtime"}
+
+
+def call(name, *args):
+    """Invoke one C-ABI entry point; non-zero status -> NativeError."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise NativeError("%s failed: %s (%d)" % (name, _ERR.get(rc, "hipError"), rc))
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(dt):
+    if dt == torch.bfloat16:
+        return DT_BF16
+    if dt == torch.float32:
+        return DT_F32
+    raise NativeError("unsupported compute dtype %s" % dt)

@@ -1,0 +1,423 @@
+// Train/eval BatchNorm (nn.BatchNorm2d semantics: biased batch variance for normalisation,
+// unbiased for running_var, momentum 0.1, eps 1e-5) over NHWC [P][C] activations, with the
+// consumers' ReLU / PReLU / residual add fused into the apply pass and the activation masks
+// fused into the backward passes.  Reference call sites: every BN in deeplab/residual_net.py
+// (:60-68,:107,:131), deeplab/deeplabv3_encoder.py (:16-32), rgbd_segmentation_RAA.py (:32-42).
+//
+// Thread layout for every kernel here: a block of 256 threads = CB chunk-columns x RPB rows,
+// each thread owns one 16-byte chunk of channels for the whole launch (so per-channel
+// constants live in registers) and walks rows with stride RPB * gridDim.y.
+#include "common.h"
+#include "../../include/cosnet_hip.h"
+
+namespace {
+
+struct Layout {
+  int CPR, CB, RPB;
+};
+template <class T> __host__ __device__ inline Layout layout_of(int C) {
+  Layout l;
+  l.CPR = C / VecOf<T>::N;
+  l.CB = l.CPR < 256 ? l.CPR : 256;
+  l.RPB = 256 / l.CB;
+  return l;
+}
+
+template <class T> __device__ __forceinline__ void ld_chunk(const T* p, float* f) {
+  Chunk<T>::unpack(*(const u32x4*)p, f);
+}
+template <class T> __device__ __forceinline__ void st_chunk(T* p, const float* f) {
+  *(u32x4*)p = Chunk<T>::pack(f);
+}
+
+// ---- forward statistics: shifted sums per thread -> (n, mean, M2) -> Chan merge ----------
+template <class T>
+__global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x, long long ld, int P,
+                                                        int C, float* __restrict__ ws) {
+  constexpr int V = VecOf<T>::N;
+  const Layout L = layout_of<T>(C);
+  const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
+  const int chunk = blockIdx.x * L.CB + tx;
+  const bool act = chunk < L.CPR && ty < L.RPB;
+  float sh[V], s[V], ss[V];
+  int n = 0;
+#pragma unroll
+  for (int v = 0; v < V; ++v) { sh[v] = 0.f; s[v] = 0.f; ss[v] = 0.f; }
+  if (act) {
+    for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
+      float f[V];
+      ld_chunk(x + (long long)r * ld + chunk * V, f);
+      if (n == 0) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) sh[v] = f[v];
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float d = f[v] - sh[v];
+        s[v] += d;
+        ss[v] = fmaf(d, d, ss[v]);
+      }
+      ++n;
+    }
+  }
+  // per-thread (mean, M2)
+  __shared__ float lm[256 * 8], l2[256 * 8];
+  __shared__ int ln[256];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    float mean = n ? sh[v] + s[v] / n : 0.f;
+    float m2 = n ? fmaxf(ss[v] - s[v] * s[v] / n, 0.f) : 0.f;
+    lm[threadIdx.x * V + v] = mean;
+    l2[threadIdx.x * V + v] = m2;
+  }
+  ln[threadIdx.x] = n;
+  __syncthreads();
+  if (ty == 0 && chunk < L.CPR) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float cn = 0.f, cm = 0.f, c2 = 0.f;
+      for (int k = 0; k < L.RPB; ++k) {
+        int t = k * L.CB + tx;
+        float nb = (float)ln[t];
+        if (nb == 0.f) continue;
+        float mb = lm[t * V + v], m2b = l2[t * V + v];
+        float nn = cn + nb, d = mb - cm;
+        cm += d * nb / nn;
+        c2 += m2b + d * d * cn * nb / nn;
+        cn = nn;
+      }
+      long long o = ((long long)blockIdx.y * C + chunk * V + v) * 3;
+      ws[o] = cn; ws[o + 1] = cm; ws[o + 2] = c2;
+    }
+  }
+}
+
+__global__ void bn_stats_finalize(const float* __restrict__ ws, int S, int C, float* mean,
+                                  float* invstd, float* run_mean, float* run_var, float momentum,
+                                  float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double cn = 0, cm = 0, c2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* w = ws + ((long long)s * C + c) * 3;
+    double nb = w[0];
+    if (nb == 0) continue;
+    double nn = cn + nb, d = w[1] - cm;
+    cm += d * nb / nn;
+    c2 += w[2] + d * d * cn * nb / nn;
+    cn = nn;
+  }
+  double var = cn > 0 ? c2 / cn : 0.0;
+  mean[c] = (float)cm;
+  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    double unb = cn > 1 ? c2 / (cn - 1) : var;
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * cm);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+  }
+}
+
+__global__ void bn_eval_params(const float* rm, const float* rv, int C, float eps, float* mean, float* invstd) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  invstd[c] = 1.0f / sqrtf(rv[c] + eps);
+}
+
+// ---- apply: y = act(bn(x) [+ res | + bn_r(xr)]) -----------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long long ldx, int P, int C,
+                                                  const float* mean, const float* invstd,
+                                                  const float* gamma, const float* beta,
+                                                  const T* __restrict__ res, long long ldr,
+                                                  const T* __restrict__ xr, long long ldxr,
+                                                  const float* rmean, const float* rinvstd,
+                                                  const float* rgamma, const float* rbeta, int act,
+                                                  const float* prelu, T* __restrict__ y,
+                                                  long long ldy) {
+  constexpr int V = VecOf<T>::N;
+  const Layout L = layout_of<T>(C);
+  const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
+  const int chunk = blockIdx.x * L.CB + tx;
+  if (chunk >= L.CPR || ty >= L.RPB) return;
+  float sc[V], sf[V], rsc[V], rsf[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    int c = chunk * V + v;
+    float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    sc[v] = g * invstd[c];
+    sf[v] = b - mean[c] * sc[v];
+    if (xr) {
+      float rg = rgamma ? rgamma[c] : 1.f, rb = rbeta ? rbeta[c] : 0.f;
+      rsc[v] = rg * rinvstd[c];
+      rsf[v] = rb - rmean[c] * rsc[v];
+    }
+  }
+  const float a = (act == 2) ? prelu[0] : 0.f;
+  for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
+    float f[V];
+    ld_chunk(x + (long long)r * ldx + chunk * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) f[v] = fmaf(f[v], sc[v], sf[v]);
+    if (res) {
+      float q[V];
+      ld_chunk(res + (long long)r * ldr + chunk * V, q);
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] += q[v];
+    }
+    if (xr) {
+      float q[V];
+      ld_chunk(xr + (long long)r * ldxr + chunk * V, q);
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] += fmaf(q[v], rsc[v], rsf[v]);
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] = fmaxf(f[v], 0.f);
+    } else if (act == 2) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] = f[v] > 0.f ? f[v] : a * f[v];
+    }
+    st_chunk(y + (long long)r * ldy + chunk * V, f);
+  }
+}
+
+// ---- backward reduce: sum(dz), sum(dz * xhat) [, sum(dy * pre * (pre<=0)) for PReLU] ------
+// dz = dy * mask, mask = (y > 0) for act 1, 1 for act 0, (pre > 0 ? 1 : a) for act 2.
+template <class T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, long long ldx,
+                                                       const T* __restrict__ dy, long long lddy,
+                                                       const T* __restrict__ y, long long ldy,
+                                                       int P, int C, const float* mean,
+                                                       const float* invstd, const float* gamma,
+                                                       const float* beta, int act,
+                                                       const float* prelu, float* __restrict__ ws) {
+  constexpr int V = VecOf<T>::N;
+  const Layout L = layout_of<T>(C);
+  const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
+  const int chunk = blockIdx.x * L.CB + tx;
+  const bool on = chunk < L.CPR && ty < L.RPB;
+  float s1[V], s2[V], s3[V], mu[V], is[V], g[V], b[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    s1[v] = s2[v] = s3[v] = 0.f;
+    int c = on ? chunk * V + v : 0;
+    mu[v] = mean[c]; is[v] = invstd[c];
+    g[v] = gamma ? gamma[c] : 1.f; b[v] = beta ? beta[c] : 0.f;
+  }
+  const float a = (act == 2) ? prelu[0] : 0.f;
+  if (on) {
+    for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
+      float xf[V], d[V];
+      ld_chunk(x + (long long)r * ldx + chunk * V, xf);
+      ld_chunk(dy + (long long)r * lddy + chunk * V, d);
+      if (act == 1) {
+        float yf[V];
+        ld_chunk(y + (long long)r * ldy + chunk * V, yf);
+#pragma unroll
+        for (int v = 0; v < V; ++v) d[v] = yf[v] > 0.f ? d[v] : 0.f;
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float xh = (xf[v] - mu[v]) * is[v];
+        if (act == 2) {
+          float pre = fmaf(xh, g[v], b[v]);
+          if (pre <= 0.f) { s3[v] = fmaf(d[v], pre, s3[v]); d[v] *= a; }
+        }
+        s1[v] += d[v];
+        s2[v] = fmaf(d[v], xh, s2[v]);
+      }
+    }
+  }
+  __shared__ float r1[256 * 8], r2[256 * 8], r3[256 * 8];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    r1[threadIdx.x * V + v] = s1[v]; r2[threadIdx.x * V + v] = s2[v]; r3[threadIdx.x * V + v] = s3[v];
+  }
+  __syncthreads();
+  if (ty == 0 && chunk < L.CPR) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      for (int k = 0; k < L.RPB; ++k) {
+        int t = (k * L.CB + tx) * V + v;
+        a1 += r1[t]; a2 += r2[t]; a3 += r3[t];
+      }
+      long long o = ((long long)blockIdx.y * C + chunk * V + v) * 3;
+      ws[o] = a1; ws[o + 1] = a2; ws[o + 2] = a3;
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize(const float* __restrict__ ws, int S, int C, float* sum_dz,
+                                float* sum_dzxh, float* dprelu_c) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0, b = 0, d = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* w = ws + ((long long)s * C + c) * 3;
+    a += w[0]; b += w[1]; d += w[2];
+  }
+  sum_dz[c] = (float)a;
+  sum_dzxh[c] = (float)b;
+  if (dprelu_c) dprelu_c[c] = (float)d;
+}
+
+// dx = gamma*invstd*(dz - sum_dz/P - xhat*sum_dzxh/P);  dres = dz (optional)
+template <class T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, long long ldx,
+                                                      const T* __restrict__ dy, long long lddy,
+                                                      const T* __restrict__ y, long long ldy,
+                                                      int P, int C, const float* mean,
+                                                      const float* invstd, const float* gamma,
+                                                      const float* beta, int act,
+                                                      const float* prelu, const float* sum_dz,
+                                                      const float* sum_dzxh, T* __restrict__ dx,
+                                                      long long lddx, T* __restrict__ dres,
+                                                      long long lddres) {
+  constexpr int V = VecOf<T>::N;
+  const Layout L = layout_of<T>(C);
+  const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
+  const int chunk = blockIdx.x * L.CB + tx;
+  if (chunk >= L.CPR || ty >= L.RPB) return;
+  float mu[V], is[V], k1[V], m1[V], m2[V], g[V], b[V];
+  const float invP = 1.f / (float)P;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    int c = chunk * V + v;
+    mu[v] = mean[c]; is[v] = invstd[c];
+    g[v] = gamma ? gamma[c] : 1.f; b[v] = beta ? beta[c] : 0.f;
+    k1[v] = g[v] * is[v];
+    m1[v] = sum_dz[c] * invP;
+    m2[v] = sum_dzxh[c] * invP;
+  }
+  const float a = (act == 2) ? prelu[0] : 0.f;
+  for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
+    float xf[V], d[V];
+    ld_chunk(x + (long long)r * ldx + chunk * V, xf);
+    ld_chunk(dy + (long long)r * lddy + chunk * V, d);
+    if (act == 1) {
+      float yf[V];
+      ld_chunk(y + (long long)r * ldy + chunk * V, yf);
+#pragma unroll
+      for (int v = 0; v < V; ++v) d[v] = yf[v] > 0.f ? d[v] : 0.f;
+    }
+    float o[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float xh = (xf[v] - mu[v]) * is[v];
+      if (act == 2) {
+        float pre = fmaf(xh, g[v], b[v]);
+        if (pre <= 0.f) d[v] *= a;
+      }
+      o[v] = k1[v] * (d[v] - m1[v] - xh * m2[v]);
+    }
+    st_chunk(dx + (long long)r * lddx + chunk * V, o);
+    if (dres) st_chunk(dres + (long long)r * lddres + chunk * V, d);
+  }
+}
+
+template <class T> int grid_rows(int P, int C, int* gx) {
+  Layout L = layout_of<T>(C);
+  *gx = (L.CPR + L.CB - 1) / L.CB;
+  int want = (2048 + *gx - 1) / *gx;             // ~2048 blocks
+  int maxy = (P + L.RPB - 1) / L.RPB;
+  int gy = want < maxy ? want : maxy;
+  return gy < 1 ? 1 : gy;
+}
+
+template <class T> int splits_for(int P, int C) {
+  int gx;
+  int gy = grid_rows<T>(P, C, &gx);
+  return gy;
+}
+
+}  // namespace
+
+extern "C" size_t cn_bn_workspace_floats(int dtype, int P, int C) {
+  int S = dtype == DT_BF16 ? splits_for<bf16>(P, C) : splits_for<float>(P, C);
+  return (size_t)S * C * 3;
+}
+
+extern "C" int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int C, float* mean,
+                           float* invstd, float* run_mean, float* run_var, float momentum,
+                           float eps, float* ws, hipStream_t st) {
+  if (C % (dtype == DT_BF16 ? 8 : 4) || ldx % (dtype == DT_BF16 ? 8 : 4)) return CN_ERR_ALIGN;
+  int gx, gy;
+  if (dtype == DT_BF16) {
+    gy = grid_rows<bf16>(P, C, &gx);
+    hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C, ws);
+  } else {
+    gy = grid_rows<float>(P, C, &gx);
+    hipLaunchKernelGGL(bn_stats_partial<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C, ws);
+  }
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 255) / 256), dim3(256), 0, st, ws, gy, C, mean,
+                     invstd, run_mean, run_var, momentum, eps);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps,
+                                 float* mean, float* invstd, hipStream_t st) {
+  hipLaunchKernelGGL(bn_eval_params, dim3((C + 255) / 256), dim3(256), 0, st, run_mean, run_var, C, eps, mean, invstd);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C, const float* mean,
+                           const float* invstd, const float* gamma, const float* beta,
+                           const void* res, long long ldr, const void* xr, long long ldxr,
+                           const float* rmean, const float* rinvstd, const float* rgamma,
+                           const float* rbeta, int act, const float* prelu, void* y,
+                           long long ldy, hipStream_t st) {
+  int gx, gy;
+  if (dtype == DT_BF16) {
+    gy = grid_rows<bf16>(P, C, &gx);
+    hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
+                       mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
+                       rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy);
+  } else {
+    gy = grid_rows<float>(P, C, &gx);
+    hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C,
+                       mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
+                       rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy);
+  }
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy, long long lddy,
+                         const void* y, long long ldy, int P, int C, const float* mean,
+                         const float* invstd, const float* gamma, const float* beta, int act,
+                         const float* prelu, float* dgamma, float* dbeta, float* dprelu_c,
+                         void* dx, long long lddx, void* dres, long long lddres, float* ws,
+                         hipStream_t st) {
+  int gx, gy;
+  if (dtype == DT_BF16) {
+    gy = grid_rows<bf16>(P, C, &gx);
+    hipLaunchKernelGGL(bn_bwd_reduce_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
+                       (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,
+                       act, prelu, ws);
+  } else {
+    gy = grid_rows<float>(P, C, &gx);
+    hipLaunchKernelGGL(bn_bwd_reduce_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
+                       (const float*)dy, lddy, (const float*)y, ldy, P, C, mean, invstd, gamma,
+                       beta, act, prelu, ws);
+  }
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
+  CN_CHECK_LAUNCH();
+  if (!dx) return 0;
+  if (dtype == DT_BF16) {
+    hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
+                       (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,
+                       act, prelu, dbeta, dgamma, (bf16*)dx, lddx, (bf16*)dres, lddres);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
+                       (const float*)dy, lddy, (const float*)y, ldy, P, C, mean, invstd, gamma,
+                       beta, act, prelu, dbeta, dgamma, (float*)dx, lddx, (float*)dres, lddres);
+  }
+  CN_CHECK_LAUNCH();
+  return 0;
+}

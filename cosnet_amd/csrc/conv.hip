@@ -1,0 +1,149 @@
+// C-ABI entry points of the convolution / matrix-product family.  Each maps one reference
+// aten call onto the implicit-GEMM kernel in gemm.hip (see include/cosnet_hip.h).
+#include "gemm.h"
+#include "../../include/cosnet_hip.h"
+
+static GemmArgs gemm_defaults() {
+  GemmArgs a = {};
+  a.nsplit = 1;
+  a.k_chunk = 1 << 30;
+  a.alpha = 1.f;
+  FastDiv one = fastdiv_make(1);
+  a.ga.div_C = a.ga.div_KW = a.ga.div_OW = a.ga.div_OHW = one;
+  a.gb = a.ga;
+  a.rm_div_OW = a.rm_div_OHW = one;
+  return a;
+}
+
+static ConvGeom make_geom(int N, int H, int W, int C, int OH, int OW, int KH, int KW, int st,
+                          int off_y, int off_x, int step_y, int step_x) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.OH = OH; g.OW = OW; g.KH = KH; g.KW = KW; g.st = st;
+  g.off_y = off_y; g.off_x = off_x; g.step_y = step_y; g.step_x = step_x;
+  g.div_C = fastdiv_make(C);
+  g.div_KW = fastdiv_make(KW);
+  g.div_OW = fastdiv_make(OW);
+  g.div_OHW = fastdiv_make(OH * OW);
+  return g;
+}
+
+static int vec_of(int dtype) { return dtype == DT_BF16 ? 8 : 4; }
+
+extern "C" int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                           const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                           const float* bias, void* y, long long ldy, int OH, int OW,
+                           hipStream_t st) {
+  if (Cin % vec_of(dtype) || ldx % vec_of(dtype)) return CN_ERR_ALIGN;
+  if (OH != (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  if (OW != (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  GemmArgs a = gemm_defaults();
+  a.M = N * OH * OW; a.N = Cout; a.K = KH * KW * Cin;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = x; a.lda = ldx;
+  a.B = w; a.ldb = a.K;
+  a.C = y; a.ldc = ldy;
+  a.bias = bias;
+  int la = L_KC_CONV;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) la = L_KC_DENSE;
+  else a.ga = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  return cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
+}
+
+extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, int OH, int OW,
+                             int Cout, const void* wt, int Cin, int KH, int KW, int stride,
+                             int pad, int dil, void* dx, long long lddx, int H, int W,
+                             int accumulate, hipStream_t st) {
+  if (Cout % vec_of(dtype) || lddy % vec_of(dtype)) return CN_ERR_ALIGN;
+  GemmArgs a = gemm_defaults();
+  a.N = Cin; a.K = KH * KW * Cout;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = dy; a.lda = lddy;
+  a.B = wt; a.ldb = a.K;
+  a.C = dx; a.ldc = lddx;
+  a.c_mode = accumulate ? 2 : 0;
+  if (stride == 1) {
+    a.M = N * H * W;
+    int la = L_KC_DENSE;
+    if (!(KH == 1 && KW == 1 && pad == 0)) {
+      la = L_KC_CONV;  // dX[n,h,w] = sum_{r,s} dY[n, h + pad - r*dil, w + pad - s*dil] . W[r,s]
+      a.ga = make_geom(N, OH, OW, Cout, H, W, KH, KW, 1, pad, pad, -dil, -dil);
+    }
+    return cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
+  }
+  if (KH != 1 || KW != 1 || pad != 0) return CN_ERR_UNSUPPORTED;
+  if (stride != 2) return CN_ERR_UNSUPPORTED;
+  // 1x1 stride 2: only input pixels (2oy, 2ox) receive gradient; zero the rest first
+  // (unless accumulating into an existing gradient).
+  if (!accumulate) {
+    if (lddx != Cin) return CN_ERR_ALIGN;
+    size_t bytes = (size_t)N * H * W * Cin * (dtype == DT_BF16 ? 2 : 4);
+    if (hipMemsetAsync(dx, 0, bytes, st) != hipSuccess) return CN_ERR_HIP;
+  }
+  a.M = N * OH * OW;
+  a.row_map = 1;
+  a.rm_div_OW = fastdiv_make(OW);
+  a.rm_div_OHW = fastdiv_make(OH * OW);
+  a.rm_H = H; a.rm_W = W;
+  return cn_gemm_dispatch(a, dtype, 0, L_KC_DENSE, L_KC_DENSE, 1, st);
+}
+
+static int pick_splits(int tiles, int K, int BK) {
+  // aim for ~2 waves of 256 CUs, keep each split >= 4 K-tiles
+  int want = (512 + tiles - 1) / tiles;
+  int maxs = K / (4 * BK);
+  if (maxs < 1) maxs = 1;
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  return want;
+}
+
+extern "C" int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                             const void* dy, long long lddy, int OH, int OW, int Cout, int KH,
+                             int KW, int stride, int pad, int dil, float* dw, hipStream_t st) {
+  if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
+  GemmArgs a = gemm_defaults();
+  a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = dy; a.lda = lddy;
+  a.B = x; a.ldb = ldx;
+  a.C = dw; a.ldc = a.N;
+  a.c_mode = 1;  // fp32 atomics (split-K); dw must be zeroed by the caller
+  int lb = L_MC_DENSE;
+  if (!(KH == 1 && KW == 1 && stride == 1 && pad == 0)) {
+    lb = L_MC_CONV;
+    a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  }
+  int BK = 8 * vec_of(dtype);
+  int tiles = ((a.M + 127) / 128) * ((a.N + (a.N <= 64 ? 63 : 127)) / (a.N <= 64 ? 64 : 128));
+  int ns = pick_splits(tiles, a.K, BK);
+  int chunk = (a.K + ns - 1) / ns;
+  chunk = (chunk + BK - 1) / BK * BK;
+  a.nsplit = (a.K + chunk - 1) / chunk;
+  a.k_chunk = chunk;
+  return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, 1, st);
+}
+
+extern "C" int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int K, int ka_lim,
+                       int kb_lim, const void* A, long long lda, long long a_bs, const void* B,
+                       long long ldb, long long b_bs, void* C, long long ldc, long long c_bs,
+                       int c_f32, int c_mode, float alpha, const float* bias, int batch,
+                       int nsplit, hipStream_t st) {
+  GemmArgs a = gemm_defaults();
+  a.M = M; a.N = N; a.K = K;
+  a.ka_lim = ka_lim; a.kb_lim = kb_lim;
+  a.A = A; a.lda = lda; a.a_bs = a_bs;
+  a.B = B; a.ldb = ldb; a.b_bs = b_bs;
+  a.C = C; a.ldc = ldc; a.c_bs = c_bs;
+  a.bias = bias;
+  a.alpha = alpha;
+  a.c_mode = c_mode;
+  if (c_mode == 1 && !c_f32) return CN_ERR_UNSUPPORTED;
+  if (nsplit > 1) {
+    int BK = 8 * vec_of(dtype);
+    int chunk = (K + nsplit - 1) / nsplit;
+    chunk = (chunk + BK - 1) / BK * BK;
+    a.nsplit = (K + chunk - 1) / chunk;
+    a.k_chunk = chunk;
+  }
+  return cn_gemm_dispatch(a, dtype, c_f32, layout_a, layout_b, batch, st);
+}

@@ -1,0 +1,723 @@
+// Memory-bound kernels of the hot path: layout conversion, weight preparation, pooling,
+// gating, decoder head, bilinear upsample + sigmoid, loss, SGD.  All NHWC [P][C] with row
+// stride ld; 16-byte vector accesses wherever channels are contiguous.
+#include "common.h"
+#include "../../include/cosnet_hip.h"
+
+namespace {
+
+template <class T> __device__ __forceinline__ void ldv(const T* p, float* f) {
+  Chunk<T>::unpack(*(const u32x4*)p, f);
+}
+template <class T> __device__ __forceinline__ void stv(T* p, const float* f) {
+  *(u32x4*)p = Chunk<T>::pack(f);
+}
+
+// ---- input: NCHW fp32 -> NHWC T with channels zero-padded to Cp ------------------------
+template <class T>
+__global__ void nchw_to_nhwc_k(const float* __restrict__ x, int N, int C, int H, int W, int Cp,
+                               T* __restrict__ y) {
+  long long total = (long long)N * H * W;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    long long n = p / ((long long)H * W), hw = p - n * H * W;
+    for (int c = 0; c < Cp; ++c) {
+      float v = c < C ? x[(n * C + c) * H * W + hw] : 0.f;
+      y[p * Cp + c] = fromf<T>(v);
+    }
+  }
+}
+
+// ---- weights: fp32 [Cout][KHW][Cin] -> T [Cout][KHW][Cp] and T [Cin][KHW][Cout] ---------
+template <class T>
+__global__ void weight_prep_k(const float* __restrict__ w, int Cout, int KHW, int Cin, int Cp,
+                              T* __restrict__ wf, T* __restrict__ wt) {
+  long long total = (long long)Cout * KHW * Cp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int ci = (int)(i % Cp);
+    long long rest = i / Cp;
+    int t = (int)(rest % KHW);
+    int co = (int)(rest / KHW);
+    float v = ci < Cin ? w[((long long)co * KHW + t) * Cin + ci] : 0.f;
+    wf[i] = fromf<T>(v);
+    if (wt && ci < Cin) wt[((long long)ci * KHW + t) * Cout + co] = fromf<T>(v);
+  }
+}
+
+// ---- max pool 3x3 / s2 / p1 / ceil_mode (deeplab/residual_net.py:109) -------------------
+template <class T>
+__global__ void maxpool_fwd_k(const T* __restrict__ x, int N, int H, int W, int C, int OH, int OW,
+                              int k, int s, int pad, T* __restrict__ y, unsigned char* __restrict__ am) {
+  constexpr int V = VecOf<T>::N;
+  const int CPR = C / V;
+  long long total = (long long)N * OH * OW * CPR;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int cc = (int)(i % CPR);
+    long long p = i / CPR;
+    int ox = (int)(p % OW);
+    long long q = p / OW;
+    int oy = (int)(q % OH);
+    int n = (int)(q / OH);
+    float best[V];
+    int bi[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) { best[v] = -INFINITY; bi[v] = 0; }
+    for (int r = 0; r < k; ++r) {
+      int yy = oy * s - pad + r;
+      if (yy < 0 || yy >= H) continue;
+      for (int c = 0; c < k; ++c) {
+        int xx = ox * s - pad + c;
+        if (xx < 0 || xx >= W) continue;
+        float f[V];
+        ldv(x + (((long long)n * H + yy) * W + xx) * C + cc * V, f);
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (f[v] > best[v] || (f[v] != f[v])) { best[v] = f[v]; bi[v] = r * k + c; }
+      }
+    }
+    stv(y + p * C + cc * V, best);
+#pragma unroll
+    for (int v = 0; v < V; ++v) am[p * C + cc * V + v] = (unsigned char)bi[v];
+  }
+}
+
+// gather form: each input pixel sums the outputs whose argmax points at it (deterministic)
+template <class T>
+__global__ void maxpool_bwd_k(const T* __restrict__ dy, const unsigned char* __restrict__ am,
+                              int N, int H, int W, int C, int OH, int OW, int k, int s, int pad,
+                              T* __restrict__ dx) {
+  constexpr int V = VecOf<T>::N;
+  const int CPR = C / V;
+  long long total = (long long)N * H * W * CPR;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int cc = (int)(i % CPR);
+    long long p = i / CPR;
+    int xx = (int)(p % W);
+    long long q = p / W;
+    int yy = (int)(q % H);
+    int n = (int)(q / H);
+    float acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = 0.f;
+    // outputs oy with oy*s - pad <= yy <= oy*s - pad + k - 1
+    int oy_lo = (yy + pad - (k - 1) + s - 1) / s; if (yy + pad - (k - 1) < 0) oy_lo = 0;
+    int oy_hi = (yy + pad) / s; if (oy_hi > OH - 1) oy_hi = OH - 1;
+    int ox_lo = (xx + pad - (k - 1) + s - 1) / s; if (xx + pad - (k - 1) < 0) ox_lo = 0;
+    int ox_hi = (xx + pad) / s; if (ox_hi > OW - 1) ox_hi = OW - 1;
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      int r = yy - (oy * s - pad);
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        int c = xx - (ox * s - pad);
+        int idx = r * k + c;
+        long long o = (((long long)n * OH + oy) * OW + ox) * C + cc * V;
+        float g[V];
+        ldv(dy + o, g);
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (am[o + v] == idx) acc[v] += g[v];
+      }
+    }
+    stv(dx + p * C + cc * V, acc);
+  }
+}
+
+// ---- global average pool over HW per image: T [N*HW][C] (ld) -> T [N][C] --------------
+template <class T>
+__global__ void avgpool_k(const T* __restrict__ x, long long ld, int HW, int C, float scale,
+                          T* __restrict__ y) {
+  // grid (C/VEC chunks / 64, N); block 256 = 64 chunks x 4 row groups
+  constexpr int V = VecOf<T>::N;
+  int cc = blockIdx.x * 64 + (threadIdx.x & 63);
+  int rg = threadIdx.x >> 6;
+  int n = blockIdx.y;
+  __shared__ float red[4][64][8];
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+  if (cc * V < C) {
+    for (int r = rg; r < HW; r += 4) {
+      float f[V];
+      ldv(x + ((long long)n * HW + r) * ld + cc * V, f);
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] += f[v];
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[rg][threadIdx.x & 63][v] = acc[v];
+  __syncthreads();
+  if (rg == 0 && cc * V < C) {
+    float o[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      o[v] = (red[0][threadIdx.x][v] + red[1][threadIdx.x][v] + red[2][threadIdx.x][v] +
+              red[3][threadIdx.x][v]) * scale;
+    stv(y + (long long)n * C + cc * V, o);
+  }
+}
+
+// broadcast T [N][C] over HW rows into dst (ld); scale applied (1 for fwd, 1/HW for avgpool bwd)
+template <class T>
+__global__ void bcast_rows_k(const T* __restrict__ src, int N, int HW, int C, float scale,
+                             T* __restrict__ dst, long long ld, int accumulate) {
+  constexpr int V = VecOf<T>::N;
+  const int CPR = C / V;
+  long long total = (long long)N * HW * CPR;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int cc = (int)(i % CPR);
+    long long p = i / CPR;
+    int n = (int)(p / HW);
+    float f[V];
+    ldv(src + (long long)n * C + cc * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) f[v] *= scale;
+    if (accumulate) {
+      float q[V];
+      ldv(dst + p * ld + cc * V, q);
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] += q[v];
+    }
+    stv(dst + p * ld + cc * V, f);
+  }
+}
+
+// ---- spatial gate: m = sigmoid(z . g + b); out = z * m  (rgbd_segmentation_RAA.py:177-184)
+// one wave per pixel row
+template <class T>
+__global__ void gate_fwd_k(const T* __restrict__ z, long long ldz, int P, int C,
+                           const float* __restrict__ g, const float* __restrict__ gb,
+                           T* __restrict__ out, long long ldo, float* __restrict__ mask) {
+  constexpr int V = VecOf<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= P) return;
+  const int CPR = C / V;
+  float acc = 0.f;
+  for (int cc = lane; cc < CPR; cc += 64) {
+    float f[V];
+    ldv(z + (long long)row * ldz + cc * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc = fmaf(f[v], g[cc * V + v], acc);
+  }
+  acc = warp_sum(acc);
+  float m = 1.f / (1.f + expf(-(acc + (gb ? gb[0] : 0.f))));
+  if (lane == 0 && mask) mask[row] = m;
+  for (int cc = lane; cc < CPR; cc += 64) {
+    float f[V];
+    ldv(z + (long long)row * ldz + cc * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) f[v] *= m;
+    stv(out + (long long)row * ldo + cc * V, f);
+  }
+}
+
+// dz = dout*m + (sum_c dout*z) * m(1-m) * g ;  dg += sum_p (.)*z ; dgb += sum_p (.)
+template <class T>
+__global__ void gate_bwd_k(const T* __restrict__ z, long long ldz, const T* __restrict__ dout,
+                           long long lddo, const float* __restrict__ mask, int P, int C,
+                           const float* __restrict__ g, int through_mask, T* __restrict__ dz,
+                           long long lddz, float* __restrict__ dg, float* __restrict__ dgb) {
+  constexpr int V = VecOf<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int CPR = C / V;
+  if (row >= P) return;
+  float dm = 0.f;
+  for (int cc = through_mask ? lane : CPR; cc < CPR; cc += 64) {
+    float f[V], d[V];
+    ldv(z + (long long)row * ldz + cc * V, f);
+    ldv(dout + (long long)row * lddo + cc * V, d);
+#pragma unroll
+    for (int v = 0; v < V; ++v) dm = fmaf(f[v], d[v], dm);
+  }
+  dm = warp_sum(dm);
+  const float m = mask[row];
+  const float dpre = dm * m * (1.f - m);
+  if (lane == 0 && dgb) atomicAdd(dgb, dpre);
+  for (int cc = lane; cc < CPR; cc += 64) {
+    float f[V], d[V], o[V];
+    ldv(z + (long long)row * ldz + cc * V, f);
+    ldv(dout + (long long)row * lddo + cc * V, d);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      o[v] = d[v] * m + dpre * g[cc * V + v];
+      if (dg) atomicAdd(dg + cc * V + v, dpre * f[v]);
+    }
+    stv(dz + (long long)row * lddz + cc * V, o);
+  }
+}
+
+// ---- decoder head: zr = relu(a [+ b]) (stored if zout), logit = zr . w + bias ---------------
+template <class T>
+__global__ void head_fwd_k(const T* __restrict__ a, long long lda, const T* __restrict__ b,
+                           long long ldb, int P, int C, int relu, const float* __restrict__ w,
+                           const float* __restrict__ bias, T* __restrict__ zout, long long ldz,
+                           float* __restrict__ logit) {
+  constexpr int V = VecOf<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= P) return;
+  const int CPR = C / V;
+  float acc = 0.f;
+  for (int cc = lane; cc < CPR; cc += 64) {
+    float f[V];
+    ldv(a + (long long)row * lda + cc * V, f);
+    if (b) {
+      float q[V];
+      ldv(b + (long long)row * ldb + cc * V, q);
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] += q[v];
+    }
+    if (relu) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] = fmaxf(f[v], 0.f);
+    }
+    if (zout) stv(zout + (long long)row * ldz + cc * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc = fmaf(f[v], w[cc * V + v], acc);
+  }
+  acc = warp_sum(acc);
+  if (lane == 0) logit[row] = acc + (bias ? bias[0] : 0.f);
+}
+
+template <class T>
+__global__ void head_bwd_k(const T* __restrict__ z, long long ldz, const float* __restrict__ dlogit,
+                           int P, int C, int relu, const float* __restrict__ w,
+                           T* __restrict__ dz, long long lddz, float* __restrict__ dw,
+                           float* __restrict__ db) {
+  constexpr int V = VecOf<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= P) return;
+  const int CPR = C / V;
+  const float dl = dlogit[row];
+  if (lane == 0 && db) atomicAdd(db, dl);
+  for (int cc = lane; cc < CPR; cc += 64) {
+    float f[V], o[V];
+    ldv(z + (long long)row * ldz + cc * V, f);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      o[v] = (!relu || f[v] > 0.f) ? dl * w[cc * V + v] : 0.f;
+      if (dw) atomicAdd(dw + cc * V + v, dl * f[v]);
+    }
+    if (dz) stv(dz + (long long)row * lddz + cc * V, o);
+  }
+}
+
+// ---- bilinear upsample (align_corners=False, torch semantics) + sigmoid ----------------
+__device__ __forceinline__ void src_index(int dst, int in, int out, float scale, int& i0, int& i1,
+                                          float& l1) {
+  float s = scale * ((float)dst + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+}
+
+__global__ void upsample_sigmoid_k(const float* __restrict__ in, int N, int h, int w, int H, int W,
+                                   float sh, float sw, int apply_sigmoid, float* __restrict__ out) {
+  long long total = (long long)N * H * W;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int X = (int)(i % W);
+    long long q = i / W;
+    int Y = (int)(q % H);
+    int n = (int)(q / H);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    src_index(Y, h, H, sh, y0, y1, ly);
+    src_index(X, w, W, sw, x0, x1, lx);
+    const float* b = in + (long long)n * h * w;
+    float v = (1.f - ly) * ((1.f - lx) * b[y0 * w + x0] + lx * b[y0 * w + x1]) +
+              ly * ((1.f - lx) * b[y1 * w + x0] + lx * b[y1 * w + x1]);
+    out[i] = apply_sigmoid ? 1.f / (1.f + expf(-v)) : v;
+  }
+}
+
+// d in[n,y,x] = sum over output pixels of dout * s(1-s) * wy * wx (gather; deterministic)
+__global__ void upsample_sigmoid_bwd_k(const float* __restrict__ dout, const float* __restrict__ out,
+                                       int N, int h, int w, int H, int W, float sh, float sw,
+                                       int apply_sigmoid, float* __restrict__ din) {
+  long long total = (long long)N * h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int x = (int)(i % w);
+    long long q = i / w;
+    int y = (int)(q % h);
+    int n = (int)(q / h);
+    // output rows Y whose source interval touches y: src(Y) in (y-1, y+1)
+    int Ylo = (int)floorf(((float)y - 1.f + 0.5f) / sh - 0.5f) - 1;
+    int Yhi = (int)ceilf(((float)y + 1.f + 0.5f) / sh - 0.5f) + 1;
+    int Xlo = (int)floorf(((float)x - 1.f + 0.5f) / sw - 0.5f) - 1;
+    int Xhi = (int)ceilf(((float)x + 1.f + 0.5f) / sw - 0.5f) + 1;
+    if (Ylo < 0) Ylo = 0;
+    if (Xlo < 0) Xlo = 0;
+    if (Yhi > H - 1) Yhi = H - 1;
+    if (Xhi > W - 1) Xhi = W - 1;
+    float acc = 0.f;
+    for (int Y = Ylo; Y <= Yhi; ++Y) {
+      int y0, y1;
+      float ly;
+      src_index(Y, h, H, sh, y0, y1, ly);
+      float wy = (y0 == y ? 1.f - ly : 0.f) + (y1 == y ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int X = Xlo; X <= Xhi; ++X) {
+        int x0, x1;
+        float lx;
+        src_index(X, w, W, sw, x0, x1, lx);
+        float wx = (x0 == x ? 1.f - lx : 0.f) + (x1 == x ? lx : 0.f);
+        if (wx == 0.f) continue;
+        long long o = ((long long)n * H + Y) * W + X;
+        float g = dout[o];
+        if (apply_sigmoid) { float s = out[o]; g *= s * (1.f - s); }
+        acc = fmaf(g, wy * wx, acc);
+      }
+    }
+    din[i] = acc;
+  }
+}
+
+// ---- loss: r*BCE + 0.8*L1 (train.py:176-216), gradient fused --------------------------
+__global__ void count_ge_k(const float* __restrict__ gt, long long n, float thr, unsigned long long* cnt) {
+  unsigned long long c = 0;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    c += gt[i] >= thr ? 1ull : 0ull;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+// partial[block] = sum of per-element loss; dpred = d loss / d pred (already / n, * gscale)
+__global__ void bce_l1_k(const float* __restrict__ p, const float* __restrict__ y, long long n,
+                         float weight, float l1w, float* __restrict__ partial,
+                         float* __restrict__ dpred) {
+  float acc = 0.f;
+  const float invn = 1.f / (float)n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float pv = p[i], yv = y[i];
+    float lp = fmaxf(logf(pv), -100.f), l1p = fmaxf(logf(1.f - pv), -100.f);
+    float bce = -weight * (yv * lp + (1.f - yv) * l1p);
+    float d = pv - yv;
+    acc += bce + l1w * fabsf(d);
+    if (dpred) {
+      float gb = weight * d / fmaxf((1.f - pv) * pv, 1e-12f);
+      float gl = l1w * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+      dpred[i] = (gb + gl) * invn;
+    }
+  }
+  acc = warp_sum(acc);
+  __shared__ float s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ void sum_partials_k(const float* __restrict__ partial, int n, float scale, float* out) {
+  double a = 0;
+  for (int i = threadIdx.x; i < n; i += 64) a += partial[i];
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (threadIdx.x == 0) out[0] = (float)(a * scale);
+}
+
+// ---- SGD (torch.optim.SGD semantics: d = g + wd*p; buf = mom*buf + d (buf = d first);
+//      p -= lr * buf), multi-tensor; then refresh the compute-dtype copy ----------------------
+struct SgdTensor {
+  float* p;
+  const float* g;
+  float* buf;
+  long long n;
+  int group;
+  int first;
+};
+
+__global__ void sgd_k(const SgdTensor* __restrict__ ts, int nt, const float* __restrict__ lrs,
+                      float wd, float mom) {
+  for (int t = blockIdx.y; t < nt; t += gridDim.y) {
+    SgdTensor T = ts[t];
+    if (!T.g) continue;
+    float lr = lrs[T.group];
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < T.n;
+         i += (long long)gridDim.x * blockDim.x) {
+      float d = T.g[i] + wd * T.p[i];
+      float b = T.first ? d : fmaf(mom, T.buf[i], d);
+      T.buf[i] = b;
+      T.p[i] -= lr * b;
+    }
+  }
+}
+
+// ---- generic helpers ------------------------------------------------------------------
+template <class T>
+__global__ void rowdot_k(const T* __restrict__ a, long long lda, const T* __restrict__ b,
+                         long long ldb, int P, int C, float* __restrict__ out) {
+  constexpr int V = VecOf<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= P) return;
+  float acc = 0.f;
+  for (int cc = lane; cc < C / V; cc += 64) {
+    float f[V], q[V];
+    ldv(a + (long long)row * lda + cc * V, f);
+    ldv(b + (long long)row * ldb + cc * V, q);
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc = fmaf(f[v], q[v], acc);
+  }
+  acc = warp_sum(acc);
+  if (lane == 0) out[row] = acc;
+}
+
+// column sums of T [P][C] (ld) into fp32 [C] (atomic across row blocks)
+template <class T>
+__global__ void colsum_k(const T* __restrict__ x, long long ld, int P, int C, float* __restrict__ out) {
+  constexpr int V = VecOf<T>::N;
+  int cc = blockIdx.x * 64 + (threadIdx.x & 63);
+  int rg = threadIdx.x >> 6;
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+  if (cc * V < C) {
+    for (int r = blockIdx.y * 4 + rg; r < P; r += gridDim.y * 4) {
+      float f[V];
+      ldv(x + (long long)r * ld + cc * V, f);
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] += f[v];
+    }
+  }
+  __shared__ float red[4][64][8];
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[rg][threadIdx.x & 63][v] = acc[v];
+  __syncthreads();
+  if (rg == 0 && cc * V < C) {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      atomicAdd(out + cc * V + v, red[0][threadIdx.x][v] + red[1][threadIdx.x][v] +
+                                      red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
+  }
+}
+
+template <class TI, class TO>
+__global__ void cast2d_k(const TI* __restrict__ x, long long ldx, int P, int C, TO* __restrict__ y,
+                         long long ldy, int accumulate) {
+  long long total = (long long)P * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long r = i / C;
+    int c = (int)(i - r * C);
+    float v = tof(x[r * ldx + c]);
+    if (accumulate) v += tof(y[r * ldy + c]);
+    y[r * ldy + c] = fromf<TO>(v);
+  }
+}
+
+inline int nblocks(long long n, int per = 256) {
+  long long b = (n + per - 1) / per;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+extern "C" int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp,
+                               void* y, hipStream_t st) {
+  long long n = (long long)N * H * W;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, x, N, C, H, W, Cp, (bf16*)y);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_k<float>, dim3(nblocks(n)), dim3(256), 0, st, x, N, C, H, W, Cp, (float*)y);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_weight_prep(int dtype, const float* w, int Cout, int KHW, int Cin, int Cp,
+                              void* wf, void* wt, hipStream_t st) {
+  long long n = (long long)Cout * KHW * Cp;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(weight_prep_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, w, Cout, KHW, Cin, Cp, (bf16*)wf, (bf16*)wt);
+  else
+    hipLaunchKernelGGL(weight_prep_k<float>, dim3(nblocks(n)), dim3(256), 0, st, w, Cout, KHW, Cin, Cp, (float*)wf, (float*)wt);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int OH, int OW,
+                              int k, int s, int pad, void* y, unsigned char* argmax, hipStream_t st) {
+  long long n = (long long)N * OH * OW * (C / (dtype == DT_BF16 ? 8 : 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, (const bf16*)x, N, H, W, C, OH, OW, k, s, pad, (bf16*)y, argmax);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_k<float>, dim3(nblocks(n)), dim3(256), 0, st, (const float*)x, N, H, W, C, OH, OW, k, s, pad, (float*)y, argmax);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* argmax, int N, int H,
+                              int W, int C, int OH, int OW, int k, int s, int pad, void* dx,
+                              hipStream_t st) {
+  long long n = (long long)N * H * W * (C / (dtype == DT_BF16 ? 8 : 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, (const bf16*)dy, argmax, N, H, W, C, OH, OW, k, s, pad, (bf16*)dx);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_k<float>, dim3(nblocks(n)), dim3(256), 0, st, (const float*)dy, argmax, N, H, W, C, OH, OW, k, s, pad, (float*)dx);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C,
+                          float scale, void* y, hipStream_t st) {
+  int V = dtype == DT_BF16 ? 8 : 4;
+  dim3 grid((C / V + 63) / 64, N);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(avgpool_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, HW, C, scale, (bf16*)y);
+  else
+    hipLaunchKernelGGL(avgpool_k<float>, grid, dim3(256), 0, st, (const float*)x, ld, HW, C, scale, (float*)y);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bcast_rows(int dtype, const void* src, int N, int HW, int C, float scale,
+                             void* dst, long long ld, int accumulate, hipStream_t st) {
+  long long n = (long long)N * HW * (C / (dtype == DT_BF16 ? 8 : 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(bcast_rows_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, (const bf16*)src, N, HW, C, scale, (bf16*)dst, ld, accumulate);
+  else
+    hipLaunchKernelGGL(bcast_rows_k<float>, dim3(nblocks(n)), dim3(256), 0, st, (const float*)src, N, HW, C, scale, (float*)dst, ld, accumulate);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_gate_fwd(int dtype, const void* z, long long ldz, int P, int C, const float* g,
+                           const float* gb, void* out, long long ldo, float* mask, hipStream_t st) {
+  dim3 grid((P + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gate_fwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, P, C, g, gb, (bf16*)out, ldo, mask);
+  else
+    hipLaunchKernelGGL(gate_fwd_k<float>, grid, dim3(256), 0, st, (const float*)z, ldz, P, C, g, gb, (float*)out, ldo, mask);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
+                           const float* mask, int P, int C, const float* g, int through_mask,
+                           void* dz, long long lddz, float* dg, float* dgb, hipStream_t st) {
+  dim3 grid((P + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gate_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, (const bf16*)dout, lddo, mask, P, C, g, through_mask, (bf16*)dz, lddz, dg, dgb);
+  else
+    hipLaunchKernelGGL(gate_bwd_k<float>, grid, dim3(256), 0, st, (const float*)z, ldz, (const float*)dout, lddo, mask, P, C, g, through_mask, (float*)dz, lddz, dg, dgb);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_head_fwd(int dtype, const void* a, long long lda, const void* b, long long ldb,
+                           int P, int C, int relu, const float* w, const float* bias, void* zout,
+                           long long ldz, float* logit, hipStream_t st) {
+  dim3 grid((P + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(head_fwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, P, C, relu, w, bias, (bf16*)zout, ldz, logit);
+  else
+    hipLaunchKernelGGL(head_fwd_k<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, P, C, relu, w, bias, (float*)zout, ldz, logit);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_head_bwd(int dtype, const void* z, long long ldz, const float* dlogit, int P, int C,
+                           int relu, const float* w, void* dz, long long lddz, float* dw, float* db,
+                           hipStream_t st) {
+  dim3 grid((P + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(head_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, dlogit, P, C, relu, w, (bf16*)dz, lddz, dw, db);
+  else
+    hipLaunchKernelGGL(head_bwd_k<float>, grid, dim3(256), 0, st, (const float*)z, ldz, dlogit, P, C, relu, w, (float*)dz, lddz, dw, db);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_upsample_sigmoid(const float* in, int N, int h, int w, int H, int W,
+                                   int apply_sigmoid, float* out, hipStream_t st) {
+  float sh = (float)h / (float)H, sw = (float)w / (float)W;
+  long long n = (long long)N * H * W;
+  hipLaunchKernelGGL(upsample_sigmoid_k, dim3(nblocks(n)), dim3(256), 0, st, in, N, h, w, H, W, sh, sw, apply_sigmoid, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_upsample_sigmoid_bwd(const float* dout, const float* out, int N, int h, int w,
+                                       int H, int W, int apply_sigmoid, float* din, hipStream_t st) {
+  float sh = (float)h / (float)H, sw = (float)w / (float)W;
+  long long n = (long long)N * h * w;
+  hipLaunchKernelGGL(upsample_sigmoid_bwd_k, dim3(nblocks(n)), dim3(256), 0, st, dout, out, N, h, w, H, W, sh, sw, apply_sigmoid, din);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_count_ge(const float* gt, long long n, float thr, unsigned long long* cnt, hipStream_t st) {
+  if (hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st) != hipSuccess) return CN_ERR_HIP;
+  hipLaunchKernelGGL(count_ge_k, dim3(nblocks(n)), dim3(256), 0, st, gt, n, thr, cnt);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" size_t cn_loss_workspace_floats(long long n) { return (size_t)nblocks(n, 1024); }
+
+extern "C" int cn_bce_l1(const float* pred, const float* gt, long long n, float weight, float l1w,
+                         float* ws, float* loss, float* dpred, hipStream_t st) {
+  int nb = nblocks(n, 1024);
+  hipLaunchKernelGGL(bce_l1_k, dim3(nb), dim3(256), 0, st, pred, gt, n, weight, l1w, ws, dpred);
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials_k, dim3(1), dim3(64), 0, st, ws, nb, 1.0f / (float)n, loss);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float momentum,
+                      hipStream_t st) {
+  dim3 grid(64, nt < 1024 ? nt : 1024);
+  hipLaunchKernelGGL(sgd_k, grid, dim3(256), 0, st, (const SgdTensor*)tensors, nt, lrs, wd, momentum);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb,
+                         int P, int C, float* out, hipStream_t st) {
+  dim3 grid((P + 3) / 4);
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(rowdot_k<bf16>, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, P, C, out);
+  else
+    hipLaunchKernelGGL(rowdot_k<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, P, C, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
+                         hipStream_t st) {
+  int V = dtype == DT_BF16 ? 8 : 4;
+  int gx = (C / V + 63) / 64;
+  int gy = (P + 63) / 64;
+  if (gy > 256) gy = 256;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(colsum_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ld, P, C, out);
+  else
+    hipLaunchKernelGGL(colsum_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ld, P, C, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C,
+                         void* y, long long ldy, int accumulate, hipStream_t st) {
+  int nb = nblocks((long long)P * C);
+  if (dtype_in == DT_F32 && dtype_out == DT_BF16)
+    hipLaunchKernelGGL((cast2d_k<float, bf16>), dim3(nb), dim3(256), 0, st, (const float*)x, ldx, P, C, (bf16*)y, ldy, accumulate);
+  else if (dtype_in == DT_BF16 && dtype_out == DT_F32)
+    hipLaunchKernelGGL((cast2d_k<bf16, float>), dim3(nb), dim3(256), 0, st, (const bf16*)x, ldx, P, C, (float*)y, ldy, accumulate);
+  else if (dtype_in == DT_F32)
+    hipLaunchKernelGGL((cast2d_k<float, float>), dim3(nb), dim3(256), 0, st, (const float*)x, ldx, P, C, (float*)y, ldy, accumulate);
+  else
+    hipLaunchKernelGGL((cast2d_k<bf16, bf16>), dim3(nb), dim3(256), 0, st, (const bf16*)x, ldx, P, C, (bf16*)y, ldy, accumulate);
+  CN_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,38 @@
+// Argument block of the generic implicit-GEMM kernel (gemm.hip).
+#pragma once
+#include "common.h"
+
+enum LoadKind { L_KC_DENSE = 0, L_KC_CONV = 1, L_MC_DENSE = 2, L_MC_CONV = 3 };
+
+// Gather geometry.  For a KC_CONV A operand the GEMM row m is an output pixel (n, oy, ox)
+// over the (OH, OW) grid and k = (r, s, ci); the source element is
+//   src[n, oy*st + off_y + r*step_y, ox*st + off_x + s*step_x, ci]  (zero outside H x W).
+// Forward conv:  st = stride, off = -pad, step = +dilation.
+// Dgrad (stride 1): src = dY, off = +pad, step = -dilation, weights in [Cin][kh][kw][Cout].
+// For an MC_CONV B operand (wgrad) k is the output pixel and n = (r, s, ci).
+struct ConvGeom {
+  int N, H, W, C;
+  int OH, OW;
+  int KH, KW;
+  int st;
+  int off_y, off_x, step_y, step_x;
+  FastDiv div_C, div_KW, div_OW, div_OHW;
+};
+
+struct GemmArgs {
+  int M, N, K;
+  int ka_lim, kb_lim;          // k validity bound of each operand (zero beyond)
+  const void* A; long long lda, a_bs;
+  const void* B; long long ldb, b_bs;
+  void* C; long long ldc, c_bs;
+  const float* bias;           // [N] fp32 or null
+  ConvGeom ga, gb;
+  int k_chunk, nsplit;         // split-K: blockIdx.z = batch * nsplit + split
+  int row_map;                 // 1: stride-2 dgrad scatter of output rows
+  FastDiv rm_div_OW, rm_div_OHW;
+  int rm_H, rm_W;
+  int c_mode;                  // 0 store, 1 fp32 atomic add, 2 read-add-store
+  float alpha;
+};
+
+int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);

@@ -1,0 +1,382 @@
+// Generic implicit-GEMM on MFMA for gfx950 (CDNA4).
+//
+//   C[m][n] = alpha * sum_k A[m][k] * B[n][k]  (+ bias[n])   with fp32 accumulation
+//
+// Every matrix product on the hot path is an instance of this one kernel; the operands are
+// produced by "loaders" that gather straight from NHWC activations, so no im2col buffer is
+// ever materialised:
+//   KC_DENSE : A/B row-major with k contiguous (weights [Cout][kh][kw][Cin], features [HW][C])
+//   KC_CONV  : rows = output pixels, k = (r, s, ci) gathered from an NHWC tensor
+//              (conv forward; conv dgrad with stride 1 is the same gather with negated taps)
+//   MC_DENSE : k-major source, m/n contiguous (dY [P][Cout] in wgrad, V [HW][C] in attention)
+//   MC_CONV  : k = output pixel, n = (r, s, ci) gathered from NHWC input (wgrad B operand)
+// KC tiles live in LDS as [rows][128 B] with a (row & 7) XOR swizzle of the 16-B chunks, read
+// with ds_read_b128; MC tiles live as [k][cols] and are read with the gfx950 hardware
+// transpose read ds_read_b64_tr_b16 (bf16) or scalar reads (fp32 parity path).
+// Block = 256 threads = 4 waves in a 2x2 grid, each wave owning a (BM/2)x(BN/2) C tile of
+// 16x16 MFMA blocks (v_mfma_f32_16x16x32_bf16, or v_mfma_f32_16x16x4_f32 for fp32).
+// K step = 128 bytes of k (64 bf16 / 32 fp32); register-staged double-buffered LDS.
+#include "common.h"
+#include "gemm.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+template <class T> struct Frag;
+template <> struct Frag<bf16> { typedef bf16x8 type; };
+template <> struct Frag<float> { typedef f32x4 type; };
+
+__device__ __forceinline__ int mc_swz(int k, int granules_per_row) {
+  // granule (8 B) XOR so that a transposed read's 32-lane half hits 32 distinct granules
+  int h = (k & 3) | (((k >> 3) & 1) << 2);
+  return (granules_per_row >= 32 ? h : (h & 3)) << 2;
+}
+
+// -------------------------------------------------------------------------------------
+// Operand loader.  ROWS = BM (A) or BN (B).  Fills `ROWS/32` 16-byte chunks per thread.
+// -------------------------------------------------------------------------------------
+template <class T, int ROWS, int KIND> struct Loader {
+  static constexpr int VEC = VecOf<T>::N;
+  static constexpr int BK = 8 * VEC;
+  static constexpr int NCH = ROWS / 32;           // chunks per thread
+  static constexpr bool MC = (KIND == L_MC_DENSE || KIND == L_MC_CONV);
+  static constexpr int CPR = ROWS / VEC;          // MC: chunks per k-row
+  static constexpr int KROW_STEP = NT / CPR;      // MC: k-rows between a thread's chunks
+
+  const T* base;
+  long long ld;
+  int lim;     // row / column bound (M or N)
+  int klim;    // k bound
+  // KC_CONV per-row state
+  int img[NCH], by[NCH], bx[NCH];
+  // MC_CONV per-thread column state
+  int ci, dy, dx;
+  bool colok;
+  ConvGeom g;
+
+  __device__ __forceinline__ void init(const T* b, long long ld_, int lim_, int klim_,
+                                       const ConvGeom& geo, int origin, int tid) {
+    base = b; ld = ld_; lim = lim_; klim = klim_;
+    if (KIND == L_KC_CONV) {
+      g = geo;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int row = origin + (tid >> 3) + 32 * i;
+        int rr = row < lim ? row : 0;
+        int q, rem, oy, ox;
+        fdivmod(rr, g.div_OHW, q, rem);
+        fdivmod(rem, g.div_OW, oy, ox);
+        img[i] = row < lim ? q : -1;
+        by[i] = oy * g.st + g.off_y;
+        bx[i] = ox * g.st + g.off_x;
+      }
+    }
+    if (KIND == L_MC_CONV) {
+      g = geo;
+      int n0 = origin + (tid % CPR) * VEC;
+      colok = n0 < lim;
+      int nn = colok ? n0 : 0;
+      int tap, r, s;
+      fdivmod(nn, g.div_C, tap, ci);
+      fdivmod(tap, g.div_KW, r, s);
+      dy = r * g.step_y + g.off_y;
+      dx = s * g.step_x + g.off_x;
+    }
+  }
+
+  __device__ __forceinline__ void load(int k0, int origin, int tid, u32x4* v) const {
+    const u32x4 zero = {0u, 0u, 0u, 0u};
+    if (KIND == L_KC_DENSE) {
+      int k = k0 + (tid & 7) * VEC;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int row = origin + (tid >> 3) + 32 * i;
+        bool ok = row < lim && k < klim;
+        v[i] = ok ? *(const u32x4*)(base + (long long)row * ld + k) : zero;
+      }
+    } else if (KIND == L_KC_CONV) {
+      int k = k0 + (tid & 7) * VEC;
+      int tap, c, r, s;
+      fdivmod(k < klim ? k : 0, g.div_C, tap, c);
+      fdivmod(tap, g.div_KW, r, s);
+      int oy = r * g.step_y, ox = s * g.step_x;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int y = by[i] + oy, x = bx[i] + ox;
+        bool ok = img[i] >= 0 && k < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        long long pix = ((long long)img[i] * g.H + y) * g.W + x;
+        v[i] = ok ? *(const u32x4*)(base + pix * ld + c) : zero;
+      }
+    } else if (KIND == L_MC_DENSE) {
+      int col = origin + (tid % CPR) * VEC;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int kr = k0 + tid / CPR + KROW_STEP * i;
+        bool ok = kr < klim && col < lim;
+        v[i] = ok ? *(const u32x4*)(base + (long long)kr * ld + col) : zero;
+      }
+    } else {  // L_MC_CONV
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int p = k0 + tid / CPR + KROW_STEP * i;
+        int pp = p < klim ? p : 0;
+        int im, rem, oy, ox;
+        fdivmod(pp, g.div_OHW, im, rem);
+        fdivmod(rem, g.div_OW, oy, ox);
+        int y = oy * g.st + dy, x = ox * g.st + dx;
+        bool ok = colok && p < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        long long pix = ((long long)im * g.H + y) * g.W + x;
+        v[i] = ok ? *(const u32x4*)(base + pix * ld + ci) : zero;
+      }
+    }
+  }
+
+  // LDS image: KC -> [ROWS][128 B] swizzled; MC -> [BK][ROWS*sizeof(T)] (bf16 swizzled)
+  __device__ __forceinline__ void store(char* lds, int tid, const u32x4* v) const {
+    if (!MC) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int row = (tid >> 3) + 32 * i, c = tid & 7;
+        *(u32x4*)(lds + row * 128 + ((c ^ (row & 7)) << 4)) = v[i];
+      }
+    } else {
+      constexpr int RB = ROWS * (int)sizeof(T);  // bytes per k-row
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int kr = tid / CPR + KROW_STEP * i, cc = tid % CPR;
+        int off;
+        if (sizeof(T) == 2) {
+          int gr = (2 * cc) ^ mc_swz(kr, RB / 8);
+          off = kr * RB + gr * 8;
+        } else {
+          off = kr * RB + cc * 16;
+        }
+        *(u32x4*)(lds + off) = v[i];
+      }
+    }
+  }
+};
+
+// Fragment readers ------------------------------------------------------------------------
+// bf16: fragment for k-piece p (32 k values): lane l -> row/col (l&15), k = 32p + 8(l>>4) + j
+template <int ROWS, bool MC>
+__device__ __forceinline__ bf16x8 read_frag_bf16(const char* lds, int rowbase, int p, int lane) {
+  int g = lane >> 4;
+  if (!MC) {
+    int row = rowbase + (lane & 15);
+    int c = 4 * p + g;
+    return *(const bf16x8*)(lds + row * 128 + ((c ^ (row & 7)) << 4));
+  } else {
+    constexpr int RB = ROWS * 2;
+    int q = (lane & 15) >> 2, pp = lane & 3;
+    int gm = (rowbase >> 2) + pp;  // granule of columns rowbase + 4pp .. +3
+    int k1 = 32 * p + 8 * g + q, k2 = k1 + 4;
+    const char* a1 = lds + k1 * RB + ((gm ^ mc_swz(k1, RB / 8)) << 3);
+    const char* a2 = lds + k2 * RB + ((gm ^ mc_swz(k2, RB / 8)) << 3);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
+    typedef __attribute__((ext_vector_type(8))) short s16x8;
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+}
+
+// fp32: piece p, step j -> k = 16p + 4(l>>4) + j ; returns the 4 floats of (p) for KC,
+// or the scalar for MC (per j).
+template <int ROWS>
+__device__ __forceinline__ f32x4 read_frag_f32_kc(const char* lds, int rowbase, int p, int lane) {
+  int row = rowbase + (lane & 15);
+  int c = 4 * p + (lane >> 4);
+  return *(const f32x4*)(lds + row * 128 + ((c ^ (row & 7)) << 4));
+}
+template <int ROWS>
+__device__ __forceinline__ float read_frag_f32_mc(const char* lds, int rowbase, int p, int j, int lane) {
+  int k = 16 * p + 4 * (lane >> 4) + j;
+  int col = rowbase + (lane & 15);
+  return *(const float*)(lds + k * (ROWS * 4) + col * 4);
+}
+
+template <class CT> __device__ __forceinline__ void store_c(CT* c, float v, int mode);
+template <> __device__ __forceinline__ void store_c<float>(float* c, float v, int mode) {
+  if (mode == 1) atomicAdd(c, v);
+  else if (mode == 2) *c += v;
+  else *c = v;
+}
+template <> __device__ __forceinline__ void store_c<bf16>(bf16* c, float v, int mode) {
+  if (mode == 2) v += (float)*c;
+  *c = (bf16)v;
+}
+
+}  // namespace
+
+template <class T, class CT, int BM, int BN, int LA, int LB>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
+  constexpr int VEC = VecOf<T>::N;
+  constexpr int BK = 8 * VEC;
+  constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
+  constexpr int STAGE = ABYTES + BBYTES;
+  constexpr int RM = BM / 32, RN = BN / 32;  // 16x16 blocks per wave in m / n
+  constexpr bool AMC = (LA == L_MC_DENSE || LA == L_MC_CONV);
+  constexpr bool BMC = (LB == L_MC_DENSE || LB == L_MC_CONV);
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int bz = blockIdx.z;
+  const int batch = bz / p.nsplit, split = bz - batch * p.nsplit;
+  const int kbeg = split * p.k_chunk;
+  const int kend = min(p.K, kbeg + p.k_chunk);
+  const int nt = (kend - kbeg + BK - 1) / BK;
+
+  const T* Abase = (const T*)p.A + (long long)batch * p.a_bs;
+  const T* Bbase = (const T*)p.B + (long long)batch * p.b_bs;
+
+  Loader<T, BM, LA> la;
+  Loader<T, BN, LB> lb;
+  la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid);
+  lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid);
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[BM / 32], rb[BN / 32];
+  if (nt > 0) {
+    la.load(kbeg, m0, tid, ra);
+    lb.load(kbeg, n0, tid, rb);
+    la.store(smem, tid, ra);
+    lb.store(smem + ABYTES, tid, rb);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nt;
+    if (more) {
+      la.load(kbeg + (kt + 1) * BK, m0, tid, ra);
+      lb.load(kbeg + (kt + 1) * BK, n0, tid, rb);
+    }
+    const char* As = smem + cur * STAGE;
+    const char* Bs = As + ABYTES;
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, AMC>(As, wm * (BM / 2) + i * 16, pc, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, BMC>(Bs, wn * (BN / 2) + j * 16, pc, lane);
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+        f32x4 af[RM], bfr[RN];
+        if (!AMC) {
+#pragma unroll
+          for (int i = 0; i < RM; ++i) af[i] = read_frag_f32_kc<BM>(As, wm * (BM / 2) + i * 16, pc, lane);
+        } else {
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) af[i][j] = read_frag_f32_mc<BM>(As, wm * (BM / 2) + i * 16, pc, j, lane);
+        }
+        if (!BMC) {
+#pragma unroll
+          for (int i = 0; i < RN; ++i) bfr[i] = read_frag_f32_kc<BN>(Bs, wn * (BN / 2) + i * 16, pc, lane);
+        } else {
+#pragma unroll
+          for (int i = 0; i < RN; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[i][j] = read_frag_f32_mc<BN>(Bs, wn * (BN / 2) + i * 16, pc, j, lane);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      char* nxt = smem + (cur ^ 1) * STAGE;
+      la.store(nxt, tid, ra);
+      lb.store(nxt + ABYTES, tid, rb);
+    }
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds C[4g + r][l & 15] of each 16x16 block.
+  CT* Cb = (CT*)p.C + (long long)batch * p.c_bs;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int row = m0 + wm * (BM / 2) + i * 16 + 4 * g + r;
+      if (row >= p.M) continue;
+      long long drow = row;
+      if (p.row_map == 1) {  // stride-2 dgrad scatter: row over (n, oy, ox) -> (n, 2oy, 2ox)
+        int im, rem, oy, ox;
+        fdivmod(row, p.rm_div_OHW, im, rem);
+        fdivmod(rem, p.rm_div_OW, oy, ox);
+        drow = ((long long)im * p.rm_H + 2 * oy) * p.rm_W + 2 * ox;
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        if (col >= p.N) continue;
+        float v = acc[i][j][r] * p.alpha;
+        if (p.bias) v += p.bias[col];
+        store_c<CT>(Cb + drow * p.ldc + col, v, p.c_mode);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Dispatch: choose tile by N, grid = (ceil(M/BM), ceil(N/BN), batch * nsplit)
+// ---------------------------------------------------------------------------------------
+template <class T, class CT, int BM, int BN, int LA, int LB>
+static int launch_t(const GemmArgs& a, int batch, hipStream_t st) {
+  dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, batch * a.nsplit);
+  hipLaunchKernelGGL((gemm_kernel<T, CT, BM, BN, LA, LB>), grid, dim3(NT), 0, st, a);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+template <class T, class CT, int LA, int LB>
+static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
+  if (a.N <= 64) return launch_t<T, CT, 128, 64, LA, LB>(a, batch, st);
+  return launch_t<T, CT, 128, 128, LA, LB>(a, batch, st);
+}
+
+template <class T, class CT>
+static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_t st) {
+#define CN_CASE(A_, B_) \
+  if (la == A_ && lb == B_) return launch_tile<T, CT, A_, B_>(a, batch, st);
+  CN_CASE(L_KC_DENSE, L_KC_DENSE)
+  CN_CASE(L_KC_CONV, L_KC_DENSE)
+  CN_CASE(L_KC_DENSE, L_MC_DENSE)
+  CN_CASE(L_MC_DENSE, L_MC_DENSE)
+  CN_CASE(L_MC_DENSE, L_MC_CONV)
+#undef CN_CASE
+  return -10;  // unsupported loader combination
+}
+
+int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
+  if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
+  if (dtype == DT_BF16) {
+    return c_f32 ? launch_kinds<bf16, float>(a, la, lb, batch, st)
+                 : launch_kinds<bf16, bf16>(a, la, lb, batch, st);
+  } else if (dtype == DT_F32) {
+    return launch_kinds<float, float>(a, la, lb, batch, st);
+  }
+  return -11;
+}

@@ -1,0 +1,496 @@
+"""Block-level autograd Functions: hand-written forward AND backward for each reference
+module of the hot path, every step a libcosnet_hip kernel.
+
+  StemFn        deeplab/residual_net.py:157-160   conv7x7/s2 + BN + ReLU + maxpool(ceil)
+  BottleneckFn  deeplab/residual_net.py:74-96     1x1(s) / 3x3(dil) / 1x1 + BN/ReLU + residual
+  ASPPFn        deeplab/deeplabv3_encoder.py:50-86 pool/1x1/3x3x3 branches -> cat -> 3x3 -> BN -> PReLU
+  CoattFn       rgbd_segmentation_RAA.py:150-170  linear, affinity bmm, row/col softmax, 2 gathers
+  GateCatFn     rgbd_segmentation_RAA.py:177-187  sigmoid gate, multiply, cat [Z, V]
+  ConvFn/BNFn   generic conv (+bias) and BN for the co-attention head (:188-191, :239-247)
+  HeadFn        rgbd_segmentation_RAA.py:251-261  add + ReLU + 1x1 classifier
+  UpSigFn       rgbd_segmentation_RAA.py:262-266  bilinear upsample (align_corners=False) + sigmoid
+  BceL1Fn       train.py:176-216                  r * BCE + 0.8 * L1
+
+Activations are [P, C] NHWC matrices in the model's compute dtype (bf16 or fp32); parameters
+are the fp32 masters of the nn.Module holders, gradients are produced in fp32.
+"""
+import torch
+
+from . import _native as nv
+from . import ops
+from .ops import WCACHE, bn_apply, bn_bwd, bn_stats, conv_dgrad, conv_fwd, conv_wgrad, as_param_grad
+
+F = torch.autograd.Function
+
+
+def _need(ctx):
+    return any(ctx.needs_input_grad)
+
+
+def _check_train(ctx):
+    if not ctx.training:
+        raise RuntimeError("backward through BatchNorm is implemented for train mode only")
+
+
+# ==============================================================================================
+class StemFn(F):
+    @staticmethod
+    def forward(ctx, img, mod, w, g, b):
+        n, cimg, h, wd = img.shape
+        dt = getattr(mod, "_cn_dtype", torch.bfloat16)
+        x = torch.empty((n * h * wd, 8), dtype=dt, device=img.device)
+        nv.call("cn_nchw_to_nhwc", nv.dtype_code(dt), img.data_ptr(), n, cimg, h, wd, 8,
+                x.data_ptr(), nv.stream())
+        wf, _ = WCACHE.get(w, dt, cin_pad=8, need_t=False)
+        c, oh, ow = conv_fwd(x, n, h, wd, wf, 64, 7, 2, 3, 1)
+        st = bn_stats(c, mod.bn1, mod.training)
+        y = bn_apply(c, st, mod.bn1, act=1)
+        ph, pw = ops.pool_out(oh), ops.pool_out(ow)
+        out = torch.empty((n * ph * pw, 64), dtype=dt, device=img.device)
+        am = torch.empty((n * ph * pw * 64,), dtype=torch.uint8, device=img.device)
+        nv.call("cn_maxpool_fwd", nv.dtype_code(dt), y.data_ptr(), n, oh, ow, 64, ph, pw, 3, 2, 1,
+                out.data_ptr(), am.data_ptr(), nv.stream())
+        if ctx.needs_input_grad[2]:
+            ctx.s = (x, c, y, am, st)
+        ctx.geo = (n, cimg, h, wd, oh, ow, ph, pw)
+        ctx.mod = mod
+        ctx.training = mod.training
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        _check_train(ctx)
+        x, c, y, am, st = ctx.s
+        n, cimg, h, wd, oh, ow, ph, pw = ctx.geo
+        dout = dout.contiguous()
+        dy = torch.empty_like(y)
+        nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n, oh, ow, 64, ph,
+                pw, 3, 2, 1, dy.data_ptr(), nv.stream())
+        dc, dg, db, _ = bn_bwd(c, dy, y, st, ctx.mod.bn1, act=1)
+        dw = conv_wgrad(x, n, h, wd, 8, dc, oh, ow, 64, 7, 2, 3, 1)
+        dw = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
+        return None, None, dw, dg, db
+
+
+# ==============================================================================================
+class BottleneckFn(F):
+    @staticmethod
+    def forward(ctx, x, blk, geo, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd):
+        n, h, w = geo
+        dt = x.dtype
+        tr = blk.training
+        s, d = blk.stride, blk.dilation
+        planes = w1.shape[0]
+        w1f, w1t = WCACHE.get(w1, dt)
+        w2f, w2t = WCACHE.get(w2, dt)
+        w3f, w3t = WCACHE.get(w3, dt)
+        c1, oh, ow = conv_fwd(x, n, h, w, w1f, planes, 1, s, 0, 1)
+        st1 = bn_stats(c1, blk.bn1, tr)
+        y1 = bn_apply(c1, st1, blk.bn1, act=1)
+        c2, _, _ = conv_fwd(y1, n, oh, ow, w2f, planes, 3, 1, d, d)
+        st2 = bn_stats(c2, blk.bn2, tr)
+        y2 = bn_apply(c2, st2, blk.bn2, act=1)
+        c3, _, _ = conv_fwd(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1)
+        st3 = bn_stats(c3, blk.bn3, tr)
+        cd = std = wdf = wdt = None
+        if wd is not None:
+            wdf, wdt = WCACHE.get(wd, dt)
+            bnd = blk.downsample[1]
+            cd, _, _ = conv_fwd(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1)
+            std = bn_stats(cd, bnd, tr)
+            y = bn_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd)
+        else:
+            y = bn_apply(c3, st3, blk.bn3, act=1, res=x)
+        if _need(ctx):
+            ctx.s = (x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt)
+        ctx.geo = (n, h, w, oh, ow, s, d, planes, x.shape[1])
+        ctx.blk = blk
+        ctx.training = tr
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        _check_train(ctx)
+        x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt = ctx.s
+        n, h, w, oh, ow, s, d, planes, cin = ctx.geo
+        blk = ctx.blk
+        dy = dy if dy.stride(1) == 1 else dy.contiguous()
+        has_down = cd is not None
+        need_dx = ctx.needs_input_grad[0]
+        dx = None
+        if has_down:
+            dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3, blk.bn3, act=1)
+            dcd, _, _, _ = bn_bwd(cd, dy, y, std, blk.downsample[1], act=1)
+        else:
+            dx = torch.empty_like(x)
+            dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3, blk.bn3, act=1, dres=dx)
+        dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
+        dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
+        dc2, dg2, db2, _ = bn_bwd(c2, dy2, y2, st2, blk.bn2, act=1)
+        dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
+        dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
+        dc1, dg1, db1, _ = bn_bwd(c1, dy1, y1, st1, blk.bn1, act=1)
+        dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
+        dwd = None
+        if need_dx:
+            dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
+        if has_down:
+            dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1)
+            if need_dx:
+                conv_dgrad(dcd, n, oh, ow, wdt, cin, 1, s, 0, 1, h, w, out=dx, accumulate=True)
+        W = (blk.conv1.weight, blk.conv2.weight, blk.conv3.weight)
+        gdw = as_param_grad(dwd, blk.downsample[0].weight) if has_down else None
+        return (dx if need_dx else None, None, None,
+                as_param_grad(dw1, W[0]), dg1, db1, as_param_grad(dw2, W[1]), dg2, db2,
+                as_param_grad(dw3, W[2]), dg3, db3, gdw, None, None)
+
+
+# ==============================================================================================
+class ASPPFn(F):
+    @staticmethod
+    def forward(ctx, x, mod, geo, *p):
+        (wc, bc, gx, bx, w0, b0, g0, be0, w1, b1, g1, be1, w2, b2, g2, be2, w3, b3, g3, be3,
+         wb, bb, gb, beb, pw) = p
+        n, h, w = geo
+        hw = h * w
+        P = n * hw
+        dt = x.dtype
+        tr = mod.training
+        dev = x.device
+        cat = torch.empty((P, 2560), dtype=dt, device=dev)
+        pool = torch.empty((n, 2048), dtype=dt, device=dev)
+        nv.call("cn_avgpool", ops.dtc(x), x.data_ptr(), ops.ld(x), n, hw, 2048, 1.0 / hw,
+                pool.data_ptr(), nv.stream())
+        wcf, wct = WCACHE.get(wc, dt)
+        cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=bc)
+        stp = bn_stats(cp, mod.bn_x, tr)
+        yp = bn_apply(cp, stp, mod.bn_x, act=1)
+        nv.call("cn_bcast_rows", ops.dtc(yp), yp.data_ptr(), n, hw, 512, 1.0, cat.data_ptr(), 2560, 0,
+                nv.stream())
+        convs = [(mod.conv2d_0, mod.bn_0, w0, b0, 1, 0)]
+        for i, dd in enumerate(mod.cn_dilations):
+            convs.append((getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)),
+                          (w1, w2, w3)[i], (b1, b2, b3)[i], 3, dd))
+        cs, sts, wts = [], [], []
+        for bi, (cm, bnm, wi, bi_, k, dd) in enumerate(convs):
+            wf, wt = WCACHE.get(wi, dt)
+            ci, _, _ = conv_fwd(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bias=bi_)
+            st = bn_stats(ci, bnm, tr)
+            bn_apply(ci, st, bnm, act=1, out=cat[:, 512 * (bi + 1):512 * (bi + 2)])
+            cs.append(ci)
+            sts.append(st)
+            wts.append(wt)
+        wbf, wbt = WCACHE.get(wb, dt)
+        cb, _, _ = conv_fwd(cat, n, h, w, wbf, 256, 3, 1, 1, 1, bias=bb)
+        stb = bn_stats(cb, mod.bn, tr)
+        out = bn_apply(cb, stb, mod.bn, act=2, prelu=pw)
+        if _need(ctx):
+            ctx.s = (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, pw)
+        ctx.geo = (n, h, w)
+        ctx.mod = mod
+        ctx.training = tr
+        ctx.convs = [(k, dd) for (_, _, _, _, k, dd) in convs]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        _check_train(ctx)
+        x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, pw = ctx.s
+        n, h, w = ctx.geo
+        hw = h * w
+        mod = ctx.mod
+        dout = dout if dout.stride(1) == 1 else dout.contiguous()
+        dcb, dgb, dbb, dpr = bn_bwd(cb, dout, out, stb, mod.bn, act=2, prelu=pw)
+        dwb = conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1)
+        dbias_b = ops.colsum(dcb)
+        dcat = conv_dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, 1, h, w)
+        need_dx = ctx.needs_input_grad[0]
+        dx = None
+        grads = []
+        bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
+        for bi, ((k, dd), ci, st, wt) in enumerate(zip(ctx.convs, cs, sts, wts)):
+            sl = slice(512 * (bi + 1), 512 * (bi + 2))
+            dci, dgi, dbi, _ = bn_bwd(ci, dcat[:, sl], cat[:, sl], st, bns[bi], act=1)
+            dwi = conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1))
+            dbias = ops.colsum(dci)
+            if need_dx:
+                dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
+                                accumulate=dx is not None)
+            grads.append((dwi, dbias, dgi, dbi))
+        # image-pool branch: sum over HW of its cat slice
+        dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
+        nv.call("cn_avgpool", ops.dtc(dcat), dcat.data_ptr(), ops.ld(dcat), n, hw, 512, 1.0,
+                dyp.data_ptr(), nv.stream())
+        dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp, mod.bn_x, act=1)
+        dwc = conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1)
+        dbc = ops.colsum(dcp)
+        if need_dx:
+            dpool = conv_dgrad(dcp, n, 1, 1, wct, 2048, 1, 1, 0, 1, 1, 1)
+            nv.call("cn_bcast_rows", ops.dtc(dpool), dpool.data_ptr(), n, hw, 2048, 1.0 / hw,
+                    dx.data_ptr(), ops.ld(dx), 1, nv.stream())
+        convmods = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
+        res = [dx if need_dx else None, None, None,
+               as_param_grad(dwc, mod.conv.weight), dbc, dgx, dbx]
+        for (dwi, dbias, dgi, dbi), cm in zip(grads, convmods):
+            res += [as_param_grad(dwi, cm.weight), dbias, dgi, dbi]
+        res += [as_param_grad(dwb, mod.bottleneck.weight), dbias_b, dgb, dbb, dpr]
+        return tuple(res)
+
+
+# ==============================================================================================
+class CoattFn(F):
+    """Z_a = softmax_j(S) V_b ; Z_b = softmax_i(S)^T V_a with S = (V_a W^T) V_b^T."""
+
+    @staticmethod
+    def forward(ctx, va, vb, wsim, geo):
+        n, hw = geo
+        c = va.shape[1]
+        dt = va.dtype
+        dev = va.device
+        ldp = (hw + 7) // 8 * 8
+        wf, _ = WCACHE.get(wsim, dt, need_t=False)
+        vat = ops.gemm(va, wf, n * hw, c, c, lda=ops.ld(va), ldb=c)            # :158-159
+        S = torch.empty((n, hw, ldp), dtype=torch.float32, device=dev)
+        ops.gemm(vat, vb, hw, hw, c, lda=c, ldb=ops.ld(vb), a_bs=hw * c, b_bs=hw * ops.ld(vb),
+                 out=S, ldc=ldp, c_bs=hw * ldp, batch=n)                          # :160
+        pc = torch.empty((n, hw, ldp), dtype=dt, device=dev)
+        pt = torch.empty((n, hw, ldp), dtype=dt, device=dev)
+        ws = torch.empty((int(nv.query("cn_coatt_workspace_floats", n, hw, ldp)),),
+                         dtype=torch.float32, device=dev)
+        nv.call("cn_coatt_softmax", nv.dtype_code(dt), S.data_ptr(), n, hw, ldp, pc.data_ptr(),
+                pt.data_ptr(), ws.data_ptr(), nv.stream())                        # :164-165
+        del S
+        za = ops.gemm(pc, vb, hw, c, ldp, layout_b=ops.GEMM_MC, lda=ldp, ldb=ops.ld(vb),
+                      a_bs=hw * ldp, b_bs=hw * ops.ld(vb), batch=n, kb_lim=hw)    # :170
+        zb = ops.gemm(pt, va, hw, c, ldp, layout_b=ops.GEMM_MC, lda=ldp, ldb=ops.ld(va),
+                      a_bs=hw * ldp, b_bs=hw * ops.ld(va), batch=n, kb_lim=hw)    # :169
+        if _need(ctx):
+            ctx.s = (va, vb, wf, pc, pt, za, zb)
+        ctx.geo = (n, hw, c, ldp)
+        ctx.set_materialize_grads(False)
+        return za, zb
+
+    @staticmethod
+    def backward(ctx, dza, dzb):
+        va, vb, wf, pc, pt, za, zb = ctx.s
+        n, hw, c, ldp = ctx.geo
+        dt = va.dtype
+        dev = va.device
+        P = n * hw
+        if dza is None and dzb is None:
+            return None, None, None, None
+        dza = dza.contiguous() if dza is not None else None
+        dzb = dzb.contiguous() if dzb is not None else None
+        if dza is not None:
+            dpc = torch.empty((n * hw, ldp), dtype=torch.float32, device=dev)
+            ops.gemm(dza, vb, hw, hw, c, lda=c, ldb=ops.ld(vb), a_bs=hw * c, b_bs=hw * ops.ld(vb),
+                     batch=n, out=dpc, ldc=ldp, c_bs=hw * ldp)
+            d1 = torch.empty((P,), dtype=torch.float32, device=dev)
+            nv.call("cn_rowdot", nv.dtype_code(dt), dza.data_ptr(), c, za.data_ptr(), c, P, c,
+                    d1.data_ptr(), nv.stream())
+        else:
+            dpc = torch.zeros((n * hw, ldp), dtype=torch.float32, device=dev)
+            d1 = torch.zeros((P,), dtype=torch.float32, device=dev)
+        dpr = d2 = None
+        if dzb is not None:
+            dpr = torch.empty((n * hw, ldp), dtype=torch.float32, device=dev)
+            ops.gemm(va, dzb, hw, hw, c, lda=ops.ld(va), ldb=c, a_bs=hw * ops.ld(va), b_bs=hw * c,
+                     batch=n, out=dpr, ldc=ldp, c_bs=hw * ldp)
+            d2 = torch.empty((P,), dtype=torch.float32, device=dev)
+            nv.call("cn_rowdot", nv.dtype_code(dt), dzb.data_ptr(), c, zb.data_ptr(), c, P, c,
+                    d2.data_ptr(), nv.stream())
+        ds = torch.empty((n, hw, ldp), dtype=dt, device=dev)
+        nv.call("cn_coatt_dscore", nv.dtype_code(dt), pc.data_ptr(), dpc.data_ptr(), d1.data_ptr(),
+                nv.ptr(pt if dzb is not None else None), nv.ptr(dpr), nv.ptr(d2), n, hw, ldp,
+                ds.data_ptr(), nv.stream())
+        # dVa_t = dS . Vb
+        dvat = ops.gemm(ds, vb, hw, c, ldp, layout_b=ops.GEMM_MC, lda=ldp, ldb=ops.ld(vb),
+                        a_bs=hw * ldp, b_bs=hw * ops.ld(vb), batch=n, kb_lim=hw)
+        dva = None
+        if ctx.needs_input_grad[0]:
+            dva = torch.empty((P, c), dtype=dt, device=dev)
+            mode = 0
+            if dzb is not None:  # dVa += P_row . dZb  (A = P_row[i][j] = PT[j][i], MC layout)
+                ops.gemm(pt, dzb, hw, c, hw, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=ldp,
+                         ldb=c, a_bs=hw * ldp, b_bs=hw * c, out=dva, ldc=c, c_bs=hw * c, batch=n)
+                mode = 2
+            # dVa += dVa_t . W   (B[n=ci][k=co] = W[co][ci] -> MC)
+            ops.gemm(dvat, wf, P, c, c, layout_b=ops.GEMM_MC, lda=c, ldb=c, out=dva, ldc=c,
+                     c_mode=mode)
+        dw = None
+        if ctx.needs_input_grad[2]:
+            dw = torch.zeros((c, c), dtype=torch.float32, device=dev)
+            ns = max(1, min(64, P // 512))
+            ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
+                     ldb=ops.ld(va), out=dw, ldc=c, c_mode=1, nsplit=ns)
+        return dva, None, dw, None
+
+
+# ==============================================================================================
+class GateCatFn(F):
+    """out = cat([z * sigmoid(z.g + gb), v], 1); mask constant (no_grad) for the b side."""
+
+    @staticmethod
+    def forward(ctx, z, v, g, gb, mask_const):
+        P, c = z.shape
+        dt = z.dtype
+        out = torch.empty((P, 2 * c), dtype=dt, device=z.device)
+        mask = torch.empty((P,), dtype=torch.float32, device=z.device)
+        gflat = g.reshape(-1)
+        nv.call("cn_gate_fwd", nv.dtype_code(dt), z.data_ptr(), ops.ld(z), P, c, gflat.data_ptr(),
+                nv.ptr(gb), out.data_ptr(), 2 * c, mask.data_ptr(), nv.stream())
+        ops.cast_copy(v, out[:, c:])
+        if _need(ctx):
+            ctx.s = (z, mask, gflat)
+        ctx.mask_const = mask_const
+        ctx.has_gb = gb is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        z, mask, gflat = ctx.s
+        P, c = z.shape
+        dt = z.dtype
+        dz = torch.empty_like(z)
+        through = not ctx.mask_const
+        dg = torch.zeros((c,), dtype=torch.float32, device=z.device) if through else None
+        dgb = torch.zeros((1,), dtype=torch.float32, device=z.device) if (through and ctx.has_gb) else None
+        nv.call("cn_gate_bwd", nv.dtype_code(dt), z.data_ptr(), ops.ld(z), dout.data_ptr(),
+                ops.ld(dout), mask.data_ptr(), P, c, gflat.data_ptr(), int(through), dz.data_ptr(), c,
+                nv.ptr(dg), nv.ptr(dgb), nv.stream())
+        dv = dout[:, c:] if ctx.needs_input_grad[1] else None
+        if dg is not None:
+            dg = dg.view(1, c, 1, 1)
+        return dz, dv, dg, dgb, None
+
+
+class ConvFn(F):
+    @staticmethod
+    def forward(ctx, x, w, b, geo, k, stride, pad, dil):
+        n, h, wd = geo
+        dt = x.dtype
+        wf, wt = WCACHE.get(w, dt)
+        y, oh, ow = conv_fwd(x, n, h, wd, wf, w.shape[0], k, stride, pad, dil, bias=b)
+        if _need(ctx):
+            ctx.s = (x, wt)
+        ctx.cfg = (n, h, wd, oh, ow, k, stride, pad, dil, w.shape[0], w.shape[1], b is not None)
+        ctx.w = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.s
+        n, h, wd, oh, ow, k, stride, pad, dil, cout, cin, has_b = ctx.cfg
+        dy = dy if dy.stride(1) == 1 else dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, wd)
+        dw = as_param_grad(conv_wgrad(x, n, h, wd, cin, dy, oh, ow, cout, k, stride, pad, dil), ctx.w)
+        db = ops.colsum(dy) if has_b else None
+        return dx, dw, db, None, None, None, None, None
+
+
+class BNFn(F):
+    @staticmethod
+    def forward(ctx, x, g, b, bn):
+        st = bn_stats(x, bn, bn.training)
+        y = bn_apply(x, st, bn, act=0)
+        if _need(ctx):
+            ctx.s = (x, st)
+        ctx.bn = bn
+        ctx.training = bn.training
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        _check_train(ctx)
+        x, st = ctx.s
+        dy = dy if dy.stride(1) == 1 else dy.contiguous()
+        dx, dg, db, _ = bn_bwd(x, dy, None, st, ctx.bn, act=0)
+        return dx, dg, db, None
+
+
+class HeadFn(F):
+    """logit = relu(a + b) . w + bias  (b optional, relu optional) -> fp32 [P]"""
+
+    @staticmethod
+    def forward(ctx, a, b, w, bias, relu):
+        P, c = a.shape
+        dt = a.dtype
+        z = torch.empty((P, c), dtype=dt, device=a.device) if _need(ctx) else None
+        logit = torch.empty((P,), dtype=torch.float32, device=a.device)
+        wflat = w.reshape(-1)
+        nv.call("cn_head_fwd", nv.dtype_code(dt), a.data_ptr(), ops.ld(a), nv.ptr(b),
+                ops.ld(b) if b is not None else 0, P, c, int(relu), wflat.data_ptr(), nv.ptr(bias),
+                nv.ptr(z), c, logit.data_ptr(), nv.stream())
+        if z is not None:
+            ctx.s = (z, wflat)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        ctx.wshape = w.shape
+        return logit
+
+    @staticmethod
+    def backward(ctx, dlogit):
+        z, wflat = ctx.s
+        P, c = z.shape
+        dz = torch.empty_like(z)
+        dw = torch.zeros((c,), dtype=torch.float32, device=z.device)
+        db = torch.zeros((1,), dtype=torch.float32, device=z.device)
+        dlogit = dlogit.contiguous()
+        nv.call("cn_head_bwd", nv.dtype_code(z.dtype), z.data_ptr(), c, dlogit.data_ptr(), P, c,
+                int(ctx.relu), wflat.data_ptr(), dz.data_ptr(), c, dw.data_ptr(), db.data_ptr(),
+                nv.stream())
+        return dz, (dz if ctx.has_b else None), dw.view(ctx.wshape), db, None
+
+
+class UpSigFn(F):
+    @staticmethod
+    def forward(ctx, logit, geo, out_hw):
+        n, h, w = geo
+        H, W = out_hw
+        out = torch.empty((n, 1, H, W), dtype=torch.float32, device=logit.device)
+        nv.call("cn_upsample_sigmoid", logit.data_ptr(), n, h, w, H, W, 1, out.data_ptr(), nv.stream())
+        ctx.save_for_backward(out)
+        ctx.geo = (n, h, w, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        n, h, w, H, W = ctx.geo
+        dout = dout.contiguous()
+        dl = torch.empty((n * h * w,), dtype=torch.float32, device=out.device)
+        nv.call("cn_upsample_sigmoid_bwd", dout.data_ptr(), out.data_ptr(), n, h, w, H, W, 1,
+                dl.data_ptr(), nv.stream())
+        return dl, None, None
+
+
+class BceL1Fn(F):
+    """weight * BCE(pred, gt) + l1w * L1(pred, gt), means over all elements (train.py:176-216)."""
+
+    @staticmethod
+    def forward(ctx, pred, gt, weight, l1w):
+        pred = pred.contiguous()
+        gt = gt.contiguous()
+        n = pred.numel()
+        ws = torch.empty((int(nv.query("cn_loss_workspace_floats", n)),), dtype=torch.float32,
+                         device=pred.device)
+        loss = torch.empty((), dtype=torch.float32, device=pred.device)
+        dpred = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        nv.call("cn_bce_l1", pred.data_ptr(), gt.data_ptr(), n, float(weight), float(l1w),
+                ws.data_ptr(), loss.data_ptr(), nv.ptr(dpred), nv.stream())
+        ctx.dpred = dpred
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        return ctx.dpred * gout, None, None, None
+
+
+def count_positive(gt):
+    """#(gt >= 0.5) on device (int64 tensor, no host sync)."""
+    cnt = torch.empty((1,), dtype=torch.int64, device=gt.device)
+    g = gt.contiguous()
+    nv.call("cn_count_ge", g.data_ptr(), g.numel(), 0.5, cnt.data_ptr(), nv.stream())
+    return cnt

@@ -1,0 +1,207 @@
+"""Tensor-level wrappers over the C ABI (no autograd here).
+
+Activations are 2-D tensors [P, C] = NHWC flattened, possibly a channel-slice view of a
+wider buffer (row stride = t.stride(0)).  Every function launches HIP kernels from
+libcosnet_hip on the current torch stream; nothing here computes with torch ops.
+"""
+import torch
+
+from . import _native as nv
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def ld(t):
+    assert t.dim() == 2 and t.stride(1) == 1, "expected a row-major 2-D [P, C] view"
+    return t.stride(0)
+
+
+def dtc(t):
+    return nv.dtype_code(t.dtype)
+
+
+def out_hw(h, w, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1, (w + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def pool_out(h, k=3, s=2, p=1):
+    """MaxPool2d output size with ceil_mode=True (deeplab/residual_net.py:109)."""
+    o = -(-(h + 2 * p - (k - 1) - 1) // s) + 1
+    if (o - 1) * s >= h + p:
+        o -= 1
+    return o
+
+
+# ---- weights -------------------------------------------------------------------------------
+class WeightCache:
+    """Compute-dtype copies of fp32 master conv weights: [Cout][KH][KW][Cp] for the forward
+    GEMM and [Cin][KH][KW][Cout] for dgrad.  Invalidated when the parameter changes (torch
+    version counter) or when the optimizer bumps `epoch` after its in-place HIP update."""
+
+    epoch = 0
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, w, dtype, cin_pad=None, need_t=True):
+        key = (id(w), tuple(w.shape), dtype, cin_pad, need_t)
+        tag = (w._version, WeightCache.epoch, w.data_ptr())
+        hit = self._c.get(key)
+        if hit is not None and hit[0] == tag:
+            return hit[1], hit[2]
+        cout = w.shape[0]
+        cin = w.shape[1]
+        khw = w.shape[2] * w.shape[3] if w.dim() == 4 else 1
+        cp = cin_pad or cin
+        if w.dim() == 4:
+            assert w.is_contiguous(memory_format=torch.channels_last), "conv weight must be channels_last"
+        wf = torch.empty((cout, khw * cp), dtype=dtype, device=w.device)
+        wt = torch.empty((cin, khw * cout), dtype=dtype, device=w.device) if need_t else None
+        nv.call("cn_weight_prep", nv.dtype_code(dtype), w.data_ptr(), cout, khw, cin, cp,
+                wf.data_ptr(), nv.ptr(wt), nv.stream())
+        self._c[key] = (tag, wf, wt)
+        return wf, wt
+
+
+WCACHE = WeightCache()
+
+
+# ---- convolution ----------------------------------------------------------------------------
+def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
+    """x [n*h*w, >=cin] -> y [n*oh*ow, cout] (or written into `out`)."""
+    cin = wf.shape[1] // (k * k)
+    oh, ow = out_hw(h, w, k, stride, pad, dil)
+    if out is None:
+        out = torch.empty((n * oh * ow, cout), dtype=x.dtype, device=x.device)
+    nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
+            stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
+    return out, oh, ow
+
+
+def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accumulate=False):
+    cout = wt.shape[1] // (k * k)
+    if out is None:
+        out = torch.empty((n * h * w, cin), dtype=dy.dtype, device=dy.device)
+    nv.call("cn_conv_dgrad", dtc(dy), dy.data_ptr(), ld(dy), n, oh, ow, cout, wt.data_ptr(), cin,
+            k, k, stride, pad, dil, out.data_ptr(), ld(out), h, w, int(accumulate), nv.stream())
+    return out
+
+
+def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
+    """fp32 [cout, k*k*cin] weight gradient (channels_last order)."""
+    if dw is None:
+        dw = torch.zeros((cout, k * k * cin), dtype=torch.float32, device=x.device)
+    nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
+            ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.stream())
+    return dw
+
+
+def as_param_grad(dw_flat, weight):
+    """[cout, k*k*cin] fp32 (OHWI order) -> gradient shaped/stided like the channels_last param."""
+    if weight.dim() == 2:
+        return dw_flat.view(weight.shape)
+    co, ci, kh, kw = weight.shape
+    return dw_flat.view(co, kh, kw, ci).permute(0, 3, 1, 2)
+
+
+def colsum(x, out=None):
+    if out is None:
+        out = torch.zeros((x.shape[1],), dtype=torch.float32, device=x.device)
+    nv.call("cn_colsum", dtc(x), x.data_ptr(), ld(x), x.shape[0], x.shape[1], out.data_ptr(), nv.stream())
+    return out
+
+
+GEMM_KC, GEMM_MC = 0, 2
+
+
+def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, a_bs=0, b_bs=0,
+         out=None, ldc=None, c_bs=0, c_mode=0, batch=1, ka_lim=None, kb_lim=None, out_dtype=None,
+         nsplit=1, alpha=1.0, bias=None):
+    """C[m, n] = alpha * sum_k A[m, k] * B[n, k] (batched via *_bs element strides)."""
+    dt = a.dtype
+    if out is None:
+        out = torch.empty((batch * m, n), dtype=out_dtype or dt, device=a.device)
+        ldc = n
+        c_bs = m * n
+    c_f32 = int(out.dtype == torch.float32)
+    nv.call("cn_gemm", nv.dtype_code(dt), layout_a, layout_b, m, n, k,
+            k if ka_lim is None else ka_lim, k if kb_lim is None else kb_lim,
+            a.data_ptr(), lda, a_bs, b.data_ptr(), ldb, b_bs, out.data_ptr(), ldc, c_bs, c_f32,
+            c_mode, float(alpha), nv.ptr(bias), batch, nsplit, nv.stream())
+    return out
+
+
+# ---- batch norm -------------------------------------------------------------------------------
+def _ws(dtype, p, c, device):
+    n = nv.query("cn_bn_workspace_floats", nv.dtype_code(dtype), p, c)
+    return torch.empty((max(int(n), 1),), dtype=torch.float32, device=device)
+
+
+def bn_stats(x, bn, training, count_update=True):
+    """Returns (mean, invstd) fp32 [C].  Train mode updates bn.running_* (momentum 0.1)."""
+    p, c = x.shape
+    mean = torch.empty((c,), dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    if training:
+        if p <= 1:
+            raise ValueError("Expected more than 1 value per channel when training, got input size "
+                             "torch.Size([%d, %d, 1, 1])" % (p, c))
+        ws = _ws(x.dtype, p, c, x.device)
+        mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+        nv.call("cn_bn_stats", dtc(x), x.data_ptr(), ld(x), p, c, mean.data_ptr(), invstd.data_ptr(),
+                bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(mom), float(bn.eps),
+                ws.data_ptr(), nv.stream())
+        if count_update:
+            bn._cn_nbt = getattr(bn, "_cn_nbt", 0) + 1
+    else:
+        nv.call("cn_bn_eval_params", bn.running_mean.data_ptr(), bn.running_var.data_ptr(), c,
+                float(bn.eps), mean.data_ptr(), invstd.data_ptr(), nv.stream())
+    return mean, invstd
+
+
+def _affine(bn):
+    if bn.affine:
+        return bn.weight, bn.bias
+    return None, None
+
+
+def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
+    p, c = x.shape
+    if out is None:
+        out = torch.empty((p, c), dtype=x.dtype, device=x.device)
+    g, b = _affine(bn)
+    rg, rb = _affine(rbn) if rbn is not None else (None, None)
+    nv.call("cn_bn_apply", dtc(x), x.data_ptr(), ld(x), p, c, stats[0].data_ptr(), stats[1].data_ptr(),
+            nv.ptr(g), nv.ptr(b), nv.ptr(res), ld(res) if res is not None else 0, nv.ptr(xr),
+            ld(xr) if xr is not None else 0, nv.ptr(rstats[0] if rstats else None),
+            nv.ptr(rstats[1] if rstats else None), nv.ptr(rg), nv.ptr(rb), act, nv.ptr(prelu),
+            out.data_ptr(), ld(out), nv.stream())
+    return out
+
+
+def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=None):
+    """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu."""
+    p, c = x.shape
+    dgamma = torch.empty((c,), dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    dpc = torch.empty_like(dgamma) if act == 2 else None
+    if want_dx and dx is None:
+        dx = torch.empty((p, c), dtype=x.dtype, device=x.device)
+    ws = _ws(x.dtype, p, c, x.device)
+    g, b = _affine(bn)
+    nv.call("cn_bn_bwd", dtc(x), x.data_ptr(), ld(x), dy.data_ptr(), ld(dy), nv.ptr(y),
+            ld(y) if y is not None else 0, p, c, stats[0].data_ptr(), stats[1].data_ptr(), nv.ptr(g),
+            nv.ptr(b), act, nv.ptr(prelu), dgamma.data_ptr(), dbeta.data_ptr(), nv.ptr(dpc),
+            nv.ptr(dx), ld(dx) if dx is not None else 0, nv.ptr(dres),
+            ld(dres) if dres is not None else 0, ws.data_ptr(), nv.stream())
+    dprelu = None
+    if dpc is not None:
+        dprelu = dpc.sum().reshape(1)  # C=256 floats -> 1 (tiny)
+    return dx, dgamma, dbeta, dprelu
+
+
+def cast_copy(src, dst, accumulate=False):
+    nv.call("cn_cast2d", dtc(src), dtc(dst), src.data_ptr(), ld(src), src.shape[0], src.shape[1],
+            dst.data_ptr(), ld(dst), int(accumulate), nv.stream())
+    return dst

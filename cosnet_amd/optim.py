@@ -1,0 +1,125 @@
+"""SGD with momentum + weight decay as one multi-tensor HIP launch (cn_sgd), with the
+reference's two parameter groups and poly learning-rate schedule.
+
+Reference: optim.SGD([{get_1x_lr_params}, {get_10x_lr_params}], lr, momentum=0.9,
+weight_decay=5e-4) (train.py:538-540), adjust_learning_rate / lr_poly (train.py:161-174,
+:348-355), optimizer.step() (train.py:602).  Update rule = torch.optim.SGD (dampening 0,
+no nesterov): d = g + wd*p ; buf = d on the first step, else momentum*buf + d ; p -= lr*buf.
+
+`duplicate_params=True` reproduces the reference's quirk that get_1x_lr_params yields every
+RGB-encoder parameter once per enclosing module: the update is applied
+once per occurrence, in order (torch's for-loop SGD semantics).
+"""
+import struct
+
+import torch
+
+from . import _native as nv
+from .ops import WeightCache
+
+_REC = struct.Struct("<QQQqii")  # SgdTensor: p, g, buf, n, group, first
+
+
+def reference_param_groups(model, duplicate_params=False):
+    """(group0, group1) parameter lists as train.py:220-303 builds them for --model raa."""
+    g0 = []
+    for mod in model.get_params("encoder"):
+        for sub in mod.modules():
+            for p in sub.parameters():
+                if p.requires_grad:
+                    g0.append(p)
+    if not duplicate_params:
+        seen = set()
+        g0 = [p for p in g0 if not (id(p) in seen or seen.add(id(p)))]
+    g1 = []
+    for sub in ("rgb_attention", "depth", "decoder"):
+        for mod in model.get_params(sub):
+            g1.extend(mod.parameters())
+    return g0, g1
+
+
+def lr_poly(base_lr, it, max_iter, power, epoch):
+    """train.py:348-355"""
+    factor = 1 if epoch < 6 else 0.5
+    return base_lr * factor * ((1 - float(it) / max_iter) ** power)
+
+
+class SGD:
+    def __init__(self, groups, lrs, momentum=0.9, weight_decay=5e-4):
+        self.groups = [list(g) for g in groups]
+        self.lrs = list(lrs)
+        self.momentum = float(momentum)
+        self.weight_decay = float(weight_decay)
+        self.state = {}
+        self._table = None
+        self._table_key = None
+        self._lr_dev = None
+
+    def zero_grad(self, set_to_none=True):
+        for g in self.groups:
+            for p in g:
+                if p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()
+
+    def set_lrs(self, lrs):
+        self.lrs = list(lrs)
+
+    def _records(self):
+        recs, keep = [], []
+        for gi, g in enumerate(self.groups):
+            for p in g:
+                if p.grad is None:
+                    continue
+                if p.grad.dtype != torch.float32 or not _dense(p.grad, p):
+                    p.grad = p.grad.contiguous(memory_format=_fmt(p))
+                st = self.state.get(id(p))
+                first = 0
+                if st is None:
+                    st = {"momentum_buffer": torch.empty_like(p), "steps": 0}
+                    self.state[id(p)] = st
+                if st["steps"] == 0:
+                    first = 1
+                st["steps"] += 1
+                buf = st["momentum_buffer"]
+                recs.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), p.numel(), gi, first))
+                keep.append(p)
+        return recs, keep
+
+    @torch.no_grad()
+    def step(self):
+        recs, _ = self._records()
+        if not recs:
+            return
+        dev = self.groups[0][0].device if self.groups[0] else self.groups[1][0].device
+        # one launch per "generation" of first-step flags so duplicates apply sequentially
+        # (a parameter listed k times is updated k times, like torch's for-loop SGD)
+        batches, cur, seen = [], [], set()
+        for r in recs:
+            if r[0] in seen:
+                batches.append(cur)
+                cur, seen = [], set()
+            cur.append(r)
+            seen.add(r[0])
+        batches.append(cur)
+        lr = torch.tensor(self.lrs, dtype=torch.float32).to(dev, non_blocking=True)
+        self._lr_dev = lr
+        for b in batches:
+            blob = b"".join(_REC.pack(*r) for r in b)
+            tab = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev, non_blocking=True)
+            nv.call("cn_sgd", tab.data_ptr(), len(b), lr.data_ptr(), self.weight_decay,
+                    self.momentum, nv.stream())
+            self._table = tab  # keep alive until the stream consumes it
+        WeightCache.epoch += 1
+
+
+def _fmt(p):
+    if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last):
+        return torch.channels_last
+    return torch.contiguous_format
+
+
+def _dense(g, p):
+    return g.is_contiguous(memory_format=_fmt(p)) and g.stride() == p.stride()

@@ -1,0 +1,207 @@
+"""RGBDSegmentation_RAA ("ResNet + ASPP + Add") — the drop-in module of the hot path.
+
+Same class name, constructor signature, submodule/parameter names (1059 state_dict keys),
+init order, get_params / load_state and forward(rgbs_a, rgbs_b, depths_a, depths_b) ->
+(x1, x2, labels) as rgbd_segmentation_RAA.py:18-268 of the reference.  Inputs and outputs
+are fp32 NCHW on the GPU; internally every op is a libcosnet_hip kernel running on NHWC
+activations in `compute_dtype` (bf16 for throughput, fp32 for parity).
+
+Semantics kept from the reference: labels come from frame b (:146); cat order [Z, V]
+(:186); RGB gate without bias, depth gate with bias (:28, :39); the b-side gate masks are
+constants (:178-182); the whole depth b-side head is no_grad (:240-247); BN running stats
+update on both a- and b-side calls in train mode.
+"""
+import torch
+import torch.nn as nn
+
+from . import functions as fn
+from .deeplab.deeplabv3_encoder import DepthEncoder_ResNetASPP, Encoder
+
+
+class RGBDSegmentation_RAA(nn.Module):
+    def __init__(self, block, num_blocks_of_layers_4_rgb, num_blocks_of_layers_4_depth, num_classes,
+                 all_channel=256, all_dim=60 * 60, no_grad_for_counterpart=True):
+        super(RGBDSegmentation_RAA, self).__init__()
+        # RGB
+        self.encoder = Encoder(3, block, num_blocks_of_layers_4_rgb, num_classes)
+        self.rgb_similarity_weights = nn.Linear(all_channel, all_channel, bias=False)
+        self.gate = nn.Conv2d(all_channel, 1, kernel_size=1, bias=False)
+        self.gate_s = nn.Sigmoid()
+        self.reduce_channels_A = nn.Conv2d(all_channel * 2, all_channel, kernel_size=3, padding=1, bias=False)
+        self.reduce_channels_B = nn.Conv2d(all_channel * 2, all_channel, kernel_size=3, padding=1, bias=False)
+        self.bn_A = nn.BatchNorm2d(all_channel)
+        self.bn_B = nn.BatchNorm2d(all_channel)
+        self.prelu = nn.ReLU(inplace=True)
+        # Depth
+        self.depth_encoder = DepthEncoder_ResNetASPP(256, block, num_blocks_of_layers_4_depth, num_classes)
+        self.depth_similarity_weights = nn.Linear(all_channel, all_channel, bias=False)
+        self.depth_gate = nn.Conv2d(all_channel, 1, kernel_size=1, bias=True)
+        self.depth_gate_s = nn.Sigmoid()
+        self.depth_reduce_channels = nn.Conv2d(all_channel * 2, all_channel, kernel_size=3, padding=1, bias=False)
+        self.depth_bn = nn.BatchNorm2d(all_channel)
+        self.depth_weights = nn.Conv2d(all_channel, all_channel, kernel_size=1, bias=True)
+        # Decoder
+        self.segmentation_classifier_A = nn.Conv2d(all_channel, num_classes, kernel_size=1, bias=True)
+        self.segmentation_classifier_B = nn.Conv2d(all_channel, num_classes, kernel_size=1, bias=True)
+        self.softmax = nn.Sigmoid()
+        self.no_grad_for_counterpart = no_grad_for_counterpart
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                m.weight.data.normal_(0, 0.01)
+            elif isinstance(m, nn.BatchNorm2d):
+                m.weight.data.fill_(1)
+                m.bias.data.zero_()
+        if num_classes != 1:
+            raise ValueError("the HIP decoder head is built for num_classes=1 (train.py:379)")
+        self.compute_dtype = torch.bfloat16
+        self._to_channels_last()
+        self.register_state_dict_pre_hook(_flush_bn_counters)
+
+    # ---- configuration ----------------------------------------------------------------------
+    def _to_channels_last(self):
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
+
+    def set_compute_dtype(self, dtype):
+        """torch.bfloat16 (throughput) or torch.float32 (parity)."""
+        assert dtype in (torch.bfloat16, torch.float32)
+        self.compute_dtype = dtype
+        return self
+
+    def _apply(self, fn_, *a, **k):
+        r = super(RGBDSegmentation_RAA, self)._apply(fn_, *a, **k)
+        self._to_channels_last()
+        return r
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        r = super(RGBDSegmentation_RAA, self).load_state_dict(state_dict, strict=strict, assign=assign)
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m._cn_nbt = 0
+        self._to_channels_last()
+        return r
+
+    # ---- parameter groups (rgbd_segmentation_RAA.py:65-100) ----------------------------------
+    def get_params(self, subset="none"):
+        mods = []
+        if subset == "none":
+            return mods
+        if subset in ("encoder", "rgb", "all"):
+            mods.append(self.encoder)
+        if subset in ("rgb_attention", "rgb", "all"):
+            mods += [self.rgb_similarity_weights, self.gate, self.reduce_channels_A,
+                     self.reduce_channels_B, self.bn_A, self.bn_B]
+        if subset in ("depth", "all"):
+            mods.extend(self.depth_encoder.get_params())
+            mods += [self.depth_gate, self.depth_similarity_weights, self.depth_reduce_channels,
+                     self.depth_bn, self.depth_weights]
+        if subset in ("decoder", "all"):
+            mods += [self.segmentation_classifier_A, self.segmentation_classifier_B]
+        return mods
+
+    # ---- original-COSNet key remap (rgbd_segmentation_RAA.py:103-136) ----------------------
+    def load_state(self, state_dict):
+        new_params = self.state_dict().copy()
+        for k in state_dict:
+            nk = k[7:] if k.startswith("module.") else k
+            if nk.startswith("encoder.layer5."):
+                nk = nk.replace("encoder.layer5.", "encoder.aspp.")
+            elif nk.startswith("encoder.main_classifier"):
+                pass
+            elif nk.startswith("encoder."):
+                nk = nk.replace("encoder.", "encoder.backbone.")
+            elif nk.startswith("linear_e."):
+                nk = nk.replace("linear_e.", "rgb_similarity_weights.")
+            elif nk.startswith("conv1."):
+                nk = nk.replace("conv1.", "reduce_channels_A.")
+            elif nk.startswith("conv2."):
+                nk = nk.replace("conv2.", "reduce_channels_B.")
+            elif nk.startswith("bn1."):
+                nk = nk.replace("bn1.", "bn_A.")
+            elif nk.startswith("bn2."):
+                nk = nk.replace("bn2.", "bn_B.")
+            elif nk.startswith("main_classifier1."):
+                nk = nk.replace("main_classifier1.", "segmentation_classifier_A.")
+            elif nk.startswith("main_classifier2."):
+                nk = nk.replace("main_classifier2.", "segmentation_classifier_B.")
+            new_params[nk] = state_dict[k]
+        self.load_state_dict(new_params)
+
+    # ---- forward (rgbd_segmentation_RAA.py:139-268) ----------------------------------------
+    def _prep(self, t):
+        if not t.is_cuda:
+            raise RuntimeError("RGBDSegmentation_RAA (HIP) expects inputs on the GPU")
+        return t.float().contiguous()
+
+    def _set_dtype(self):
+        for m in self.modules():
+            m._cn_dtype = self.compute_dtype
+
+    def forward(self, rgbs_a, rgbs_b, depths_a, depths_b, stages=None):
+        self._set_dtype()
+        rgbs_a, rgbs_b, depths_a, depths_b = map(self._prep, (rgbs_a, rgbs_b, depths_a, depths_b))
+        input_size = tuple(rgbs_a.shape[2:])
+        ng = torch.no_grad if self.no_grad_for_counterpart else _Null
+        # RGB
+        va, geo = self.encoder.features_nhwc(rgbs_a)
+        with ng():
+            vb, _ = self.encoder.features_nhwc(rgbs_b)
+        with torch.no_grad():
+            labels = self.encoder.annotate_nhwc(vb, geo, input_size)       # frame b (:146)
+        n, h, w = geo
+        hw = h * w
+        za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw))
+        cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False)
+        cat_b = fn.GateCatFn.apply(zb, vb, self.gate.weight, None, True)  # mask_b no_grad (:178-182)
+        z_a = fn.BNFn.apply(fn.ConvFn.apply(cat_a, self.reduce_channels_A.weight, None, geo, 3, 1, 1, 1),
+                            self.bn_A.weight, self.bn_A.bias, self.bn_A)
+        z_b = fn.BNFn.apply(fn.ConvFn.apply(cat_b, self.reduce_channels_B.weight, None, geo, 3, 1, 1, 1),
+                            self.bn_B.weight, self.bn_B.bias, self.bn_B)
+        # Depth
+        da, dgeo = self.depth_encoder.features_nhwc(depths_a)
+        with ng():
+            db, _ = self.depth_encoder.features_nhwc(depths_b)
+        if dgeo != geo:
+            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+        dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw))
+        dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False)
+        dz_a = fn.BNFn.apply(fn.ConvFn.apply(dcat_a, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
+                             self.depth_bn.weight, self.depth_bn.bias, self.depth_bn)
+        dz_a = fn.ConvFn.apply(dz_a, self.depth_weights.weight, self.depth_weights.bias, geo, 1, 1, 0, 1)
+        with torch.no_grad():                                               # (:229-247)
+            dcat_b = fn.GateCatFn.apply(dzb, db, self.depth_gate.weight, self.depth_gate.bias, True)
+            dz_b = fn.BNFn.apply(fn.ConvFn.apply(dcat_b, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
+                                 self.depth_bn.weight, self.depth_bn.bias, self.depth_bn)
+            dz_b = fn.ConvFn.apply(dz_b, self.depth_weights.weight, self.depth_weights.bias, geo, 1, 1, 0, 1)
+        # fusion + decoder (:251-266)
+        la = fn.HeadFn.apply(z_a, dz_a, self.segmentation_classifier_A.weight,
+                             self.segmentation_classifier_A.bias, True)
+        lb = fn.HeadFn.apply(z_b, dz_b, self.segmentation_classifier_B.weight,
+                             self.segmentation_classifier_B.bias, True)
+        x1 = fn.UpSigFn.apply(la, geo, input_size)
+        x2 = fn.UpSigFn.apply(lb, geo, input_size)
+        if stages is not None:
+            stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
+        return x1, x2, labels
+
+
+CoattentionModel = RGBDSegmentation_RAA  # name used by BASELINE.json's north_star
+
+
+class _Null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+def _flush_bn_counters(module, prefix, keep_vars):
+    """num_batches_tracked is counted on the host during forward (no device op per BN call)
+    and folded into the buffer whenever a state_dict is taken."""
+    for m in module.modules():
+        k = getattr(m, "_cn_nbt", 0)
+        if k and isinstance(m, nn.BatchNorm2d):
+            m.num_batches_tracked.add_(k)
+            m._cn_nbt = 0

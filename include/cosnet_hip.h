@@ -1,0 +1,139 @@
+/* libcosnet_hip — C ABI of the MI355X (gfx950) hot path of RGBDSegmentation_RAA.
+ *
+ * The reference has no native code and no FFI: every entry point below
+ * replaces an implicit aten call made by the reference's Python, cited per function.
+ * Conventions
+ *   - activations are NHWC "pixel-major" matrices [P][C] with a row stride ld (elements);
+ *     a channel slice of a concat buffer is (base + offset, ld)
+ *   - dtype: 0 = fp32 (parity path), 1 = bf16 (throughput path); accumulation is fp32
+ *   - conv weights are [Cout][KH][KW][Cin] (= torch channels_last of [Cout,Cin,KH,KW]);
+ *     dgrad takes the transposed copy [Cin][KH][KW][Cout] (cn_weight_prep makes both)
+ *   - all buffers are caller-owned device memory (the library never allocates); the
+ *     *_workspace_* queries size the scratch a call needs
+ *   - every call is asynchronous on `stream`, re-entrant, never synchronises the host
+ *   - return 0 on success, a hipError_t (> 0) from the launch, or a negative CN_ERR_*;
+ *     no C++ exception crosses this boundary
+ */
+#ifndef COSNET_HIP_H
+#define COSNET_HIP_H
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CN_ERR_SHAPE (-1)
+#define CN_ERR_ALIGN (-2)
+#define CN_ERR_UNSUPPORTED (-3)
+#define CN_ERR_HIP (-4)
+
+/* ---- convolution / matrix products (implicit GEMM on MFMA) ---------------------------- */
+
+/* y = conv2d(x, w) + bias.  Replaces nn.Conv2d.forward for every conv of the path:
+ * deeplab/residual_net.py:59,63-64,67,106,129 ; deeplab/deeplabv3_encoder.py:15,19,22-31 ;
+ * rgbd_segmentation_RAA.py:30-31,41,43.  Cin % (4 fp32 | 8 bf16) == 0. */
+int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                const float* bias, void* y, long long ldy, int OH, int OW, hipStream_t stream);
+
+/* dx = conv2d input-gradient (autograd of the calls above).  stride 1: any kernel;
+ * stride 2: 1x1 / pad 0 only (deeplab/residual_net.py:59,129 of layer2 block 0). */
+int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, int OH, int OW, int Cout,
+                  const void* wt, int Cin, int KH, int KW, int stride, int pad, int dil,
+                  void* dx, long long lddx, int H, int W, int accumulate, hipStream_t stream);
+
+/* dw[Cout][KH][KW][Cin] += conv2d weight-gradient (fp32, split-K atomics; zero dw first). */
+int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                  const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
+                  int stride, int pad, int dil, float* dw, hipStream_t stream);
+
+/* Generic batched C = alpha * A . B^T (+bias) with per-operand layouts
+ * (0 = k-contiguous rows, 2 = m/n-contiguous, k-major).  Replaces the linear + bmm calls of
+ * the co-attention: rgbd_segmentation_RAA.py:159-160,169-170 (RGB) and :212-213,220-221
+ * (depth), and their autograd.  c_mode: 0 store, 1 fp32 atomic add, 2 accumulate. */
+int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int K, int ka_lim, int kb_lim,
+            const void* A, long long lda, long long a_bs, const void* B, long long ldb,
+            long long b_bs, void* C, long long ldc, long long c_bs, int c_f32, int c_mode,
+            float alpha, const float* bias, int batch, int nsplit, hipStream_t stream);
+
+/* ---- BatchNorm2d (train: batch stats + running update; eval: running stats) ---------- */
+size_t cn_bn_workspace_floats(int dtype, int P, int C);
+int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int C, float* mean, float* invstd,
+                float* run_mean, float* run_var, float momentum, float eps, float* ws,
+                hipStream_t stream);
+int cn_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps, float* mean,
+                      float* invstd, hipStream_t stream);
+/* y = act(gamma*(x-mean)*invstd + beta [+ res] [+ bn_r(xr)]); act 0 none, 1 ReLU, 2 PReLU */
+int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C, const float* mean,
+                const float* invstd, const float* gamma, const float* beta, const void* res,
+                long long ldr, const void* xr, long long ldxr, const float* rmean,
+                const float* rinvstd, const float* rgamma, const float* rbeta, int act,
+                const float* prelu, void* y, long long ldy, hipStream_t stream);
+/* backward of cn_bn_apply w.r.t. x (train mode), masks fused; dres <- dz for the residual */
+int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy, long long lddy,
+              const void* y, long long ldy, int P, int C, const float* mean, const float* invstd,
+              const float* gamma, const float* beta, int act, const float* prelu, float* dgamma,
+              float* dbeta, float* dprelu_c, void* dx, long long lddx, void* dres,
+              long long lddres, float* ws, hipStream_t stream);
+
+/* ---- co-attention softmax (rgbd_segmentation_RAA.py:164-165, :215-216) ----------------- */
+size_t cn_coatt_workspace_floats(int B, int HW, int ld);
+int cn_coatt_softmax(int dtype, const float* S, int B, int HW, int ld, void* Pc, void* PT,
+                     float* ws, hipStream_t stream);
+int cn_coatt_dscore(int dtype, const void* Pc, const float* dPc, const float* d1, const void* PT,
+                    const float* dPr, const float* d2, int B, int HW, int ld, void* dS,
+                    hipStream_t stream);
+
+/* ---- memory-bound helpers -------------------------------------------------------------- */
+int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* y,
+                    hipStream_t stream);
+int cn_weight_prep(int dtype, const float* w, int Cout, int KHW, int Cin, int Cp, void* wf,
+                   void* wt, hipStream_t stream);
+/* nn.MaxPool2d(3, 2, 1, ceil_mode=True): deeplab/residual_net.py:109,160 */
+int cn_maxpool_fwd(int dtype, const void* x, int N, int H, int W, int C, int OH, int OW, int k,
+                   int s, int pad, void* y, unsigned char* argmax, hipStream_t stream);
+int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* argmax, int N, int H, int W,
+                   int C, int OH, int OW, int k, int s, int pad, void* dx, hipStream_t stream);
+/* AdaptiveAvgPool2d(1) + 1x1 upsample broadcast: deeplab/deeplabv3_encoder.py:57-61 */
+int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C, float scale, void* y,
+               hipStream_t stream);
+int cn_bcast_rows(int dtype, const void* src, int N, int HW, int C, float scale, void* dst,
+                  long long ld, int accumulate, hipStream_t stream);
+/* gate: rgbd_segmentation_RAA.py:177-184 (RGB, no bias), :228-235 (depth, bias) */
+int cn_gate_fwd(int dtype, const void* z, long long ldz, int P, int C, const float* g,
+                const float* gb, void* out, long long ldo, float* mask, hipStream_t stream);
+int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
+                const float* mask, int P, int C, const float* g, int through_mask, void* dz,
+                long long lddz, float* dg, float* dgb, hipStream_t stream);
+/* fusion + 1x1 classifier: rgbd_segmentation_RAA.py:251-261 ; deeplabv3_encoder.py:138 */
+int cn_head_fwd(int dtype, const void* a, long long lda, const void* b, long long ldb, int P,
+                int C, int relu, const float* w, const float* bias, void* zout, long long ldz,
+                float* logit, hipStream_t stream);
+int cn_head_bwd(int dtype, const void* z, long long ldz, const float* dlogit, int P, int C,
+                int relu, const float* w, void* dz, long long lddz, float* dw, float* db,
+                hipStream_t stream);
+/* F.upsample(bilinear, align_corners=False) + sigmoid: rgbd_segmentation_RAA.py:262-266 */
+int cn_upsample_sigmoid(const float* in, int N, int h, int w, int H, int W, int apply_sigmoid,
+                        float* out, hipStream_t stream);
+int cn_upsample_sigmoid_bwd(const float* dout, const float* out, int N, int h, int w, int H,
+                            int W, int apply_sigmoid, float* din, hipStream_t stream);
+/* loss: calc_loss_BCE + 0.8 calc_loss_L1, train.py:176-216 */
+int cn_count_ge(const float* gt, long long n, float thr, unsigned long long* cnt,
+                hipStream_t stream);
+size_t cn_loss_workspace_floats(long long n);
+int cn_bce_l1(const float* pred, const float* gt, long long n, float weight, float l1w, float* ws,
+              float* loss, float* dpred, hipStream_t stream);
+/* optim.SGD(momentum, weight_decay) step over a device table of tensors: train.py:538-540,602 */
+int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float momentum,
+           hipStream_t stream);
+int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb, int P, int C,
+              float* out, hipStream_t stream);
+int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out, hipStream_t stream);
+int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C, void* y,
+              long long ldy, int accumulate, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

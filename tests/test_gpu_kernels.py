@@ -1,0 +1,350 @@
+"""Per-kernel parity on the GPU: every libcosnet_hip kernel against a plain PyTorch fp64 CPU
+restatement of the same aten op (the reference's own arithmetic), in both compute dtypes.
+
+bf16 cases round the inputs to bf16 first, so the remaining error is fp32 accumulation plus
+one bf16 output rounding: tolerance 1.2e-2 relative to the output scale; fp32 cases use the
+exact f32-input MFMA: 2e-5 relative.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from cosnet_amd import _native as nv
+from cosnet_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 1.2e-2}
+
+
+def nhwc(x):  # NCHW -> [P, C]
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def nchw(x2d, n, h, w):
+    return x2d.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def close(got, ref, dt, scale=None):
+    got = got.double().cpu()
+    ref = ref.double().cpu()
+    s = scale if scale is not None else max(ref.abs().max().item(), 1e-6)
+    err = (got - ref).abs().max().item() / s
+    assert err <= TOL[dt], "rel err %.3g > %.3g" % (err, TOL[dt])
+    return err
+
+
+def rnd(shape, dt, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g, dtype=torch.float64) * scale).to(dt).double()
+
+
+CONV_CASES = [
+    # n, cin, h, w, cout, k, stride, pad, dil
+    (2, 64, 13, 11, 128, 1, 1, 0, 1),
+    (2, 64, 13, 11, 64, 3, 1, 1, 1),
+    (2, 32, 15, 9, 64, 3, 1, 2, 2),
+    (2, 256, 7, 9, 128, 1, 2, 0, 1),
+    (2, 8, 29, 31, 64, 7, 2, 3, 1),
+    (1, 64, 9, 9, 512, 3, 1, 6, 6),
+    (1, 320, 5, 6, 256, 3, 1, 1, 1),
+    (3, 16, 4, 4, 8, 3, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(cuda, dt, case):
+    n, cin, h, w, cout, k, s, p, d = case
+    x = rnd((n, cin, h, w), dt, 1)
+    wt = rnd((cout, cin, k, k), dt, 2, scale=(2.0 / (cin * k * k)) ** 0.5)
+    b = rnd((cout,), torch.float32, 3)
+    y_ref = F.conv2d(x, wt, b, s, p, d)
+    oh, ow = y_ref.shape[2:]
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    wp = wt.float().to(cuda).contiguous(memory_format=torch.channels_last)
+    wf, wtt = ops.WCACHE.get(wp, dt)
+    y, oh2, ow2 = ops.conv_fwd(xg, n, h, w, wf, cout, k, s, p, d, bias=b.float().to(cuda))
+    assert (oh2, ow2) == (oh, ow)
+    torch.cuda.synchronize()
+    close(nchw(y, n, oh, ow), y_ref, dt)
+    # backward
+    gy = rnd(y_ref.shape, dt, 4)
+    xr = x.clone().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, s, p, d).backward(gy)
+    gyg = nhwc(gy).to(dt).to(cuda).contiguous()
+    dw = ops.conv_wgrad(xg, n, h, w, cin, gyg, oh, ow, cout, k, s, p, d)
+    torch.cuda.synchronize()
+    close(ops.as_param_grad(dw, wp), wr.grad, dt)
+    if s == 1 or k == 1:
+        dx = ops.conv_dgrad(gyg, n, oh, ow, wtt, cin, k, s, p, d, h, w)
+        torch.cuda.synchronize()
+        close(nchw(dx, n, h, w), xr.grad, dt)
+        # accumulate mode adds onto an existing gradient
+        dx2 = ops.conv_dgrad(gyg, n, oh, ow, wtt, cin, k, s, p, d, h, w, out=dx.clone(), accumulate=True)
+        torch.cuda.synchronize()
+        close(nchw(dx2, n, h, w), 2 * xr.grad, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 2), (2, 2)])
+def test_gemm_layouts_batched(cuda, dt, la, lb):
+    B, M, N, K = 3, 77, 136, 200
+    a = rnd((B, M, K), dt, 5)
+    bm = rnd((B, N, K), dt, 6)
+    ref = torch.einsum("bmk,bnk->bmn", a, bm)
+    # stored layouts: KC -> [M][K] rows; MC -> [K][M] rows (pad leading dims to multiples of 8)
+    def store(t, lay, rows):
+        if lay == 0:
+            ldv = (t.shape[2] + 7) // 8 * 8
+            buf = torch.zeros((B, t.shape[1], ldv), dtype=dt)
+            buf[:, :, :t.shape[2]] = t.to(dt)
+            return buf.to(cuda), ldv, t.shape[1] * ldv
+        ldv = (rows + 7) // 8 * 8
+        buf = torch.zeros((B, t.shape[2], ldv), dtype=dt)
+        buf[:, :, :rows] = t.transpose(1, 2).to(dt)
+        return buf.to(cuda), ldv, t.shape[2] * ldv
+    A, lda, abs_ = store(a, la, M)
+    Bt, ldb, bbs = store(bm, lb, N)
+    out = torch.empty((B * M, N), dtype=torch.float32, device=cuda)
+    ops.gemm(A, Bt, M, N, K, layout_a=la, layout_b=lb, lda=lda, ldb=ldb, a_bs=abs_, b_bs=bbs,
+             out=out, ldc=N, c_bs=M * N, batch=B)
+    torch.cuda.synchronize()
+    close(out.view(B, M, N), ref, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_atomic(cuda, dt):
+    M, N, K = 256, 192, 4000
+    a = rnd((K, M), dt, 7)
+    b = rnd((K, N), dt, 8)
+    ref = a.t() @ b
+    out = torch.zeros((M, N), dtype=torch.float32, device=cuda)
+    ops.gemm(a.to(dt).to(cuda), b.to(dt).to(cuda), M, N, K, layout_a=2, layout_b=2, lda=M, ldb=N,
+             out=out, ldc=N, c_mode=1, nsplit=7)
+    torch.cuda.synchronize()
+    close(out, ref, dt)
+
+
+def _bn_mod(c, cuda, seed):
+    bn = torch.nn.BatchNorm2d(c).to(cuda)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        bn.weight.copy_(1 + 0.1 * torch.randn(c, generator=g))
+        bn.bias.copy_(0.1 * torch.randn(c, generator=g))
+        bn.running_mean.copy_(0.2 * torch.randn(c, generator=g))
+        bn.running_var.copy_(1 + 0.3 * torch.rand(c, generator=g))
+    return bn
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("c", [64, 320, 2560])
+def test_batchnorm_train(cuda, dt, act, c):
+    n, h, w = 2, 5, 7
+    x = (rnd((n, c, h, w), dt, 9, scale=2.0) + 0.5).to(dt).double()
+    bn = _bn_mod(c, cuda, 10)
+    rm0, rv0 = bn.running_mean.double().cpu().clone(), bn.running_var.double().cpu().clone()
+    xr = x.clone().requires_grad_(True)
+    gw = bn.weight.detach().double().cpu().requires_grad_(True)
+    gb = bn.bias.detach().double().cpu().requires_grad_(True)
+    pw = torch.tensor([0.25], dtype=torch.float64, requires_grad=True)
+    rm, rv = rm0.clone(), rv0.clone()
+    y = F.batch_norm(xr, rm, rv, gw, gb, True, 0.1, 1e-5)
+    y = F.relu(y) if act == 1 else (F.prelu(y, pw) if act == 2 else y)
+    gy = rnd(y.shape, dt, 11)
+    y.backward(gy)
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    st = ops.bn_stats(xg, bn, True)
+    prelu = torch.tensor([0.25], dtype=torch.float32, device=cuda)
+    yg = ops.bn_apply(xg, st, bn, act=act, prelu=prelu)
+    torch.cuda.synchronize()
+    close(nchw(yg, n, h, w), y.detach(), dt)
+    close(bn.running_mean, rm, torch.float32, scale=1.0)
+    close(bn.running_var, rv, torch.float32, scale=1.0)
+    gyg = nhwc(gy).to(dt).to(cuda).contiguous()
+    dx, dgam, dbet, dpr = ops.bn_bwd(xg, gyg, yg, st, bn, act=act, prelu=prelu)
+    torch.cuda.synchronize()
+    close(nchw(dx, n, h, w), xr.grad, dt)
+    close(dgam, gw.grad, dt)
+    close(dbet, gb.grad, dt)
+    if act == 2:
+        close(dpr, pw.grad, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_batchnorm_residual_forms(cuda, dt):
+    n, c, h, w = 2, 64, 6, 5
+    x = rnd((n, c, h, w), dt, 12)
+    xd = rnd((n, c, h, w), dt, 13)
+    res = rnd((n, c, h, w), dt, 14)
+    bn, bnd = _bn_mod(c, cuda, 15), _bn_mod(c, cuda, 16)
+    xg, xdg, rg = (nhwc(t).to(dt).to(cuda).contiguous() for t in (x, xd, res))
+    st = ops.bn_stats(xg, bn, True)
+    std = ops.bn_stats(xdg, bnd, True)
+    y1 = ops.bn_apply(xg, st, bn, act=1, res=rg)
+    y2 = ops.bn_apply(xg, st, bn, act=1, xr=xdg, rstats=std, rbn=bnd)
+    ref_bn = lambda t, m: F.batch_norm(t, None, None, m.weight.detach().double().cpu(),
+                                       m.bias.detach().double().cpu(), True, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    close(nchw(y1, n, h, w), F.relu(ref_bn(x, bn) + res), dt)
+    close(nchw(y2, n, h, w), F.relu(ref_bn(x, bn) + ref_bn(xd, bnd)), dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_eval(cuda, dt):
+    n, c, h, w = 1, 256, 4, 6
+    x = rnd((n, c, h, w), dt, 17)
+    bn = _bn_mod(c, cuda, 18).eval()
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    st = ops.bn_stats(xg, bn, False)
+    y = ops.bn_apply(xg, st, bn, act=0)
+    ref = F.batch_norm(x, bn.running_mean.double().cpu(), bn.running_var.double().cpu(),
+                       bn.weight.detach().double().cpu(), bn.bias.detach().double().cpu(), False, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    close(nchw(y, n, h, w), ref, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(237, 237), (49, 49), (12, 17)])
+def test_maxpool_ceil(cuda, dt, hw):
+    h, w = hw
+    n, c = 2, 64
+    x = rnd((n, c, h, w), dt, 19)
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 3, 2, 1, ceil_mode=True)
+    gy = rnd(y.shape, dt, 20)
+    y.backward(gy)
+    oh, ow = ops.pool_out(h), ops.pool_out(w)
+    assert (oh, ow) == tuple(y.shape[2:])
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    out = torch.empty((n * oh * ow, c), dtype=dt, device=cuda)
+    am = torch.empty((n * oh * ow * c,), dtype=torch.uint8, device=cuda)
+    nv.call("cn_maxpool_fwd", nv.dtype_code(dt), xg.data_ptr(), n, h, w, c, oh, ow, 3, 2, 1,
+            out.data_ptr(), am.data_ptr(), nv.stream())
+    gyg = nhwc(gy).to(dt).to(cuda).contiguous()
+    dx = torch.empty_like(xg)
+    nv.call("cn_maxpool_bwd", nv.dtype_code(dt), gyg.data_ptr(), am.data_ptr(), n, h, w, c, oh, ow,
+            3, 2, 1, dx.data_ptr(), nv.stream())
+    torch.cuda.synchronize()
+    close(nchw(out, n, oh, ow), y.detach(), dt)
+    close(nchw(dx, n, h, w), xr.grad, dt)
+
+
+@pytest.mark.parametrize("hw", [((60, 60), (473, 473)), ((31, 41), (240, 320)), ((13, 13), (97, 97))])
+def test_upsample_sigmoid(cuda, hw):
+    (h, w), (H, W) = hw
+    n = 2
+    x = rnd((n, 1, h, w), torch.float32, 21, scale=3.0)
+    xr = x.clone().requires_grad_(True)
+    y = torch.sigmoid(F.interpolate(xr, size=(H, W), mode="bilinear", align_corners=False))
+    gy = rnd(y.shape, torch.float32, 22)
+    y.backward(gy)
+    xg = x.float().to(cuda).contiguous()
+    out = torch.empty((n, 1, H, W), dtype=torch.float32, device=cuda)
+    nv.call("cn_upsample_sigmoid", xg.data_ptr(), n, h, w, H, W, 1, out.data_ptr(), nv.stream())
+    din = torch.empty((n * h * w,), dtype=torch.float32, device=cuda)
+    gyg = gy.float().to(cuda).contiguous()
+    nv.call("cn_upsample_sigmoid_bwd", gyg.data_ptr(), out.data_ptr(), n, h, w, H, W, 1,
+            din.data_ptr(), nv.stream())
+    torch.cuda.synchronize()
+    close(out, y.detach(), torch.float32)
+    close(din.view(n, 1, h, w), xr.grad, torch.float32)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gate_fwd_bwd(cuda, dt, bias):
+    P, c = 333, 256
+    z = rnd((P, c), dt, 23)
+    v = rnd((P, c), dt, 24)
+    g = rnd((1, c, 1, 1), torch.float32, 25, scale=0.1)
+    gb = rnd((1,), torch.float32, 26) if bias else None
+    zr, gr = z.clone().requires_grad_(True), g.clone().requires_grad_(True)
+    gbr = gb.clone().requires_grad_(True) if bias else None
+    m = torch.sigmoid(zr @ gr.view(c, 1) + (gbr if bias else 0))
+    ref = torch.cat([zr * m, v], 1)
+    gout = rnd(ref.shape, dt, 27)
+    ref.backward(gout)
+    from cosnet_amd.functions import GateCatFn
+    zg = z.to(dt).to(cuda).requires_grad_(True)
+    vg = v.to(dt).to(cuda)
+    gg = g.float().to(cuda).requires_grad_(True)
+    gbg = gb.float().to(cuda).requires_grad_(True) if bias else None
+    out = GateCatFn.apply(zg, vg, gg, gbg, False)
+    out.backward(gout.to(dt).to(cuda))
+    torch.cuda.synchronize()
+    close(out, ref.detach(), dt)
+    close(zg.grad, zr.grad, dt)
+    close(gg.grad, gr.grad, dt)
+    if bias:
+        close(gbg.grad, gbr.grad, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_head_fwd_bwd(cuda, dt):
+    P, c = 500, 256
+    a, b = rnd((P, c), dt, 28), rnd((P, c), dt, 29)
+    w = rnd((1, c, 1, 1), torch.float32, 30, scale=0.1)
+    bias = rnd((1,), torch.float32, 31)
+    ar, br, wr, biasr = (t.clone().requires_grad_(True) for t in (a, b, w, bias))
+    ref = F.relu(ar + br) @ wr.view(c) + biasr
+    gl = rnd((P,), torch.float32, 32)
+    ref.backward(gl)
+    from cosnet_amd.functions import HeadFn
+    ag, bg = a.to(dt).to(cuda).requires_grad_(True), b.to(dt).to(cuda).requires_grad_(True)
+    wg, bsg = w.float().to(cuda).requires_grad_(True), bias.float().to(cuda).requires_grad_(True)
+    out = HeadFn.apply(ag, bg, wg, bsg, True)
+    out.backward(gl.float().to(cuda))
+    torch.cuda.synchronize()
+    close(out, ref.detach(), dt)
+    close(ag.grad, ar.grad, dt)
+    close(bg.grad, br.grad, dt)
+    close(wg.grad, wr.grad, dt)
+    close(bsg.grad, biasr.grad, dt)
+
+
+def test_loss_bce_l1(cuda):
+    from cosnet_amd import loss as L
+    g = torch.Generator().manual_seed(33)
+    pred = torch.rand((2, 1, 37, 41), generator=g, dtype=torch.float64) * 0.98 + 0.01
+    gt = (torch.rand((2, 1, 37, 41), generator=g) < 0.3).double()
+    pr = pred.clone().requires_grad_(True)
+    ratio = gt.numel() / float((gt >= 0.5).sum())
+    ref = F.binary_cross_entropy(pr, gt, weight=torch.full_like(gt, ratio)) + 0.8 * F.l1_loss(pr, gt)
+    ref.backward()
+    pg = pred.float().to(cuda).requires_grad_(True)
+    out = L.bce_l1(pg, gt.float().to(cuda))
+    out.backward()
+    torch.cuda.synchronize()
+    assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    close(pg.grad, pr.grad, torch.float32)
+    # empty GT -> unweighted BCE (train.py:185-187)
+    z = torch.zeros_like(gt)
+    ref0 = F.binary_cross_entropy(pred, z) + 0.8 * F.l1_loss(pred, z)
+    out0 = L.bce_l1(pred.float().to(cuda), z.float().to(cuda))
+    assert abs(out0.item() - ref0.item()) <= 1e-5 * abs(ref0.item())
+
+
+def test_sgd_step(cuda):
+    from cosnet_amd.optim import SGD
+    g = torch.Generator().manual_seed(34)
+    ps = [torch.randn(s, generator=g) for s in [(64, 3, 7, 7), (256,), (10, 10)]]
+    grads = [[torch.randn(p.shape, generator=g) for p in ps] for _ in range(3)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.SGD([{"params": ref[:1], "lr": 0.01}, {"params": ref[1:], "lr": 0.1}],
+                          lr=0.01, momentum=0.9, weight_decay=5e-4)
+    mine = [p.clone().to(cuda).requires_grad_(True) for p in ps]
+    mopt = SGD([mine[:1], mine[1:]], [0.01, 0.1])
+    for step in range(3):
+        for p, gr in zip(ref, grads[step]):
+            p.grad = gr.clone()
+        for p, gr in zip(mine, grads[step]):
+            p.grad = gr.clone().to(cuda)
+        opt.step()
+        mopt.step()
+    torch.cuda.synchronize()
+    for a, b in zip(mine, ref):
+        assert torch.allclose(a.detach().cpu(), b.detach(), atol=1e-6, rtol=1e-5)
