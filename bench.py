@@ -1,0 +1,179 @@
+"""Throughput benchmark of the hot path: one training step of RGBDSegmentation_RAA
+(forward of both frames x both modalities, co-attention, decoder, BCE+L1 loss, backward,
+RCCL gradient all-reduce for N > 1, SGD step) on synthetic 473x473 RGB-D frame pairs,
+batch 4 per GPU, bf16 compute (BASELINE.json configs[1]; configs[2] when launched on 8 GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  value = frame pairs per second over all ranks.
+roofline: the implicit-GEMM MFMA kernel (every conv / linear / bmm of the step): algorithmic
+FLOPs (2*M*N*K per launch) / measured launch time (HIP events on the launch stream over the
+timed steps), against the 2.5 PFLOP/s dense bf16 MFMA peak of MI355X.
+cpu_baseline: the oracle's CPU restatement (fp32 torch CPU, the reference's own op sequence)
+timed on this host on a bounded sample (one B=2 fwd+bwd step at 473x473).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFLOPS = 157.3
+FLOP_PER_PAIR_473 = 4.1364e12    # SURVEY.md §8d (flop_counter on the reference graph)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU")
+    ap.add_argument("--size", type=int, default=473)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0)")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(size):
+    """fp32 CPU oracle, B=2 train step (fwd + loss + bwd) at size x size."""
+    import torch
+    from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+    import cosnet_amd as C
+    from oracle.model_ref import RefModel, loss_bce_l1
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    tmpl = C.build_model().state_dict()
+    ref = RefModel(recipe_state_dict(tmpl), dtype=torch.float32)
+    ra, rb, da, db, ga, gb = synthetic_inputs(2, size, size, seed=99)
+    t0 = time.perf_counter()
+    x1, x2, _ = ref.forward(ra, rb, da, db)
+    loss = loss_bce_l1(x1, ga) + loss_bce_l1(x2, gb)
+    loss.backward()
+    dt = time.perf_counter() - t0
+    return {"value": 2.0 / dt, "unit": "frame-pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": "1 train step (fwd+loss+bwd), B=2 pairs at %dx%d, fp32 torch CPU restatement "
+                      "of the reference op sequence (oracle/model_ref.py); %.1f s" % (size, size, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import cosnet_amd as C
+    from cosnet_amd import loss as L
+    from cosnet_amd import ops
+    from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+    from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(1234)
+    model = C.build_model(dtype)
+    model.load_state_dict(recipe_state_dict(model.state_dict()))
+    # encoder.main_classifier only produces `labels`, which never enters the loss
+    # (SURVEY.md §3.3): it receives no gradient in the reference either.
+    model.encoder.main_classifier.requires_grad_(False)
+    model = model.to(dev).train()
+    g0, g1 = reference_param_groups(model)
+    opt = SGD([g0, g1], [0.0, 0.0], momentum=0.9, weight_decay=5e-4)
+    net = model
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[local], broadcast_buffers=True, bucket_cap_mb=64,
+            gradient_as_bucket_view=True)
+
+    B, S = args.batch, args.size
+    ra, rb, da, db, ga, gb = [t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)]
+    max_iter = 10000
+
+    def step(i):
+        lr = lr_poly(2.5e-4, i, max_iter, 0.9, 0)
+        opt.set_lrs([0.01 * lr, 10 * lr])           # train.py:171-172
+        opt.zero_grad()
+        x1, x2, _ = net(ra, rb, da, db)
+        loss = L.bce_l1(x1, ga) + L.bce_l1(x2, gb)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = ops.GemmProfile() if not args.no_roofline else None
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if prof:
+        prof.__enter__()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    if prof:
+        prof.__exit__()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    pairs = B * world * args.steps
+    out = {
+        "metric": "frame-pairs/sec (fwd+bwd) at 473x473 RGBD",
+        "value": pairs / dt,
+        "unit": "frame-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded U[0,255) BGR-mean / depth, blob masks; name-keyed random-init weights)",
+        "config": {"workload": "RGBDSegmentation_RAA train step (fwd+loss+bwd+SGD), %dx%d, "
+                               "batch %d pairs/GPU" % (S, S, B),
+                   "model": "RGBDSegmentation_RAA(Bottleneck,[3,4,23,3],[3,4,6,3],1)",
+                   "global_batch": B * world, "image_hw": [S, S], "parallelism": "dp%d" % world,
+                   "loss": float(loss.item())},
+        "model_tflops_per_s": pairs * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
+    }
+    if prof:
+        n, fl, kt = prof.summary()
+        peak = MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else MFMA_F32_PEAK_TFLOPS
+        ach = fl / kt / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv/bmm)",
+                           "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+                           "traffic": None, "launches_per_step": n / args.steps,
+                           "gemm_time_frac_of_step": kt / dt,
+                           "gemm_tflop_per_step": fl / args.steps / 1e12}
+    if rank == 0 and args.cpu_baseline and world == 1:
+        try:
+            out["cpu_baseline"] = cpu_baseline(S)
+        except Exception as e:  # report, never hide
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

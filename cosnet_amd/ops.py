@@ -33,6 +33,47 @@ def pool_out(h, k=3, s=2, p=1):
     return o
 
 
+# ---- optional per-launch timing of the implicit-GEMM kernel (bench.py roofline) -----------
+class GemmProfile:
+    """Records (algorithmic FLOPs, start, end) HIP events around every implicit-GEMM launch
+    on the current stream while active."""
+
+    active = None
+
+    def __init__(self):
+        self.rec = []
+
+    def __enter__(self):
+        GemmProfile.active = self
+        return self
+
+    def __exit__(self, *a):
+        GemmProfile.active = None
+        return False
+
+    def summary(self):
+        """(launches, total FLOPs, total kernel seconds) — call after synchronize()."""
+        fl = sum(r[0] for r in self.rec)
+        t = sum(r[1].elapsed_time(r[2]) for r in self.rec) * 1e-3
+        return len(self.rec), fl, t
+
+
+def _prof_start(flops):
+    p = GemmProfile.active
+    if p is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    p.rec.append((flops, e0, e1))
+    return e1
+
+
+def _prof_end(e1):
+    if e1 is not None:
+        e1.record()
+
+
 # ---- weights -------------------------------------------------------------------------------
 class WeightCache:
     """Compute-dtype copies of fp32 master conv weights: [Cout][KH][KW][Cp] for the forward
@@ -74,8 +115,10 @@ def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
     oh, ow = out_hw(h, w, k, stride, pad, dil)
     if out is None:
         out = torch.empty((n * oh * ow, cout), dtype=x.dtype, device=x.device)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
     nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
             stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
+    _prof_end(ev)
     return out, oh, ow
 
 
@@ -83,8 +126,10 @@ def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accu
     cout = wt.shape[1] // (k * k)
     if out is None:
         out = torch.empty((n * h * w, cin), dtype=dy.dtype, device=dy.device)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
     nv.call("cn_conv_dgrad", dtc(dy), dy.data_ptr(), ld(dy), n, oh, ow, cout, wt.data_ptr(), cin,
             k, k, stride, pad, dil, out.data_ptr(), ld(out), h, w, int(accumulate), nv.stream())
+    _prof_end(ev)
     return out
 
 
@@ -92,8 +137,10 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
     """fp32 [cout, k*k*cin] weight gradient (channels_last order)."""
     if dw is None:
         dw = torch.zeros((cout, k * k * cin), dtype=torch.float32, device=x.device)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
     nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
             ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.stream())
+    _prof_end(ev)
     return dw
 
 
@@ -125,10 +172,12 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
         ldc = n
         c_bs = m * n
     c_f32 = int(out.dtype == torch.float32)
+    ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k))
     nv.call("cn_gemm", nv.dtype_code(dt), layout_a, layout_b, m, n, k,
             k if ka_lim is None else ka_lim, k if kb_lim is None else kb_lim,
             a.data_ptr(), lda, a_bs, b.data_ptr(), ldb, b_bs, out.data_ptr(), ldc, c_bs, c_f32,
             c_mode, float(alpha), nv.ptr(bias), batch, nsplit, nv.stream())
+    _prof_end(ev)
     return out
 
 

@@ -105,7 +105,8 @@ class RefModel:
                          "depth_encoder.aspp", (2, 3, 7))
 
     # ---- rgbd_segmentation_RAA.py ----------------------------------------------------
-    def coattention(self, va, vb, w):
+    @staticmethod
+    def coattention(_self, va, vb, w):
         """rgbd_segmentation_RAA.py:150-170: returns (Z_a, Z_b) as [N, C, H, W]."""
         n, c, h, wd = va.shape
         va_f = va.reshape(n, c, h * wd)
@@ -124,7 +125,7 @@ class RefModel:
         va, labels = self.encoder(rgbs_a)
         with ng():
             vb, labels = self.encoder(rgbs_b)               # :146 labels from frame b
-        z_a, z_b = self.coattention(va, vb, self.p["rgb_similarity_weights.weight"])
+        z_a, z_b = self.coattention(self, va, vb, self.p["rgb_similarity_weights.weight"])
         m_a = torch.sigmoid(self.conv(z_a, "gate"))
         with torch.no_grad():
             m_b = torch.sigmoid(self.conv(z_b, "gate"))
@@ -136,7 +137,7 @@ class RefModel:
         da = self.depth_encoder(depths_a)
         with ng():
             db = self.depth_encoder(depths_b)
-        dz_a, dz_b = self.coattention(da, db, self.p["depth_similarity_weights.weight"])
+        dz_a, dz_b = self.coattention(self, da, db, self.p["depth_similarity_weights.weight"])
         dm_a = torch.sigmoid(self.conv(dz_a, "depth_gate"))
         with torch.no_grad():
             dm_b = torch.sigmoid(self.conv(dz_b, "depth_gate"))

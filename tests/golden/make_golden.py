@@ -155,12 +155,17 @@ def main():
         if k in ("V_b", "D_b"):
             continue
         put(arr, k, v, f64[k])
+    # the reference run entirely in bf16 (CPU): the bf16 noise floor for J-level parity
+    b16, _ = run_train(torch.bfloat16, inp)
+    for k in ("x1", "x2", "loss"):
+        arr["bf16/" + k] = b16[k].astype(np.float32)
     save("train_b2_97.npz", arr)
     meta["train_b2_97"] = {"grad_norm_keys": gkeys, "select": SELECT}
 
     # ---- 2. eval forward with calibrated BN stats --------------------------------------
     calib_in = synthetic_inputs(2, 97, 97, seed=4321)
     calib = calibrate(torch.float64, calib_in)
+    calib = {k: v.float().double() for k, v in calib.items()}  # what gets committed (fp32)
     arr = {"calib/" + k: v.float().numpy() for k, v in calib.items()}
     save("bn_calibration.npz", arr)
     for (h, w, tag) in [(97, 97, "eval_b1_97"), (240, 320, "eval_b1_240x320")]:
@@ -194,6 +199,13 @@ def main():
             for p in mod.parameters():
                 g1.append(names[id(p)])
     meta["param_groups"] = {"group0": g0, "group1": g1}
+    # ---- 3b. state_dict schema and the seeded reference init (torch.manual_seed(0)) ------
+    torch.manual_seed(0)
+    r = RGBDSegmentation_RAA(Bottleneck, [3, 4, 23, 3], [3, 4, 6, 3], num_classes=1)
+    sd = r.state_dict()
+    meta["state_dict"] = [[k, list(v.shape), str(v.dtype)] for k, v in sd.items()]
+    meta["init_seed0"] = {k: [float(v.double().sum()), float(v.double().abs().sum()),
+                              float(v.flatten()[0])] for k, v in sd.items()}
 
     # ---- 4. compute_iou known answers (evaluation.py:3-22) -----------------------------
     rng = np.random.RandomState(5)

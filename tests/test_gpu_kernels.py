@@ -348,3 +348,42 @@ def test_sgd_step(cuda):
     torch.cuda.synchronize()
     for a, b in zip(mine, ref):
         assert torch.allclose(a.detach().cpu(), b.detach(), atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("hw", [(13, 13), (15, 20), (31, 41)])
+@pytest.mark.parametrize("both", [True, False])
+def test_coattention_block(cuda, dt, hw, both):
+    """CoattFn (linear + affinity bmm + row/col softmax + 2 gathers, fwd and bwd) against the
+    oracle's restatement of rgbd_segmentation_RAA.py:150-170 in fp64.  S has std ~16 here
+    (realistic, unscaled logits).  bf16 rounds V_a W^T and P to bf16 (SURVEY.md §7 iii), so
+    its tolerance is J-level (0.15 of the output scale); fp32 is held to 2e-4."""
+    from oracle.model_ref import RefModel
+    from cosnet_amd.functions import CoattFn
+    n, c = 2, 256
+    h, w = hw
+    va = rnd((n, c, h, w), dt, 40)
+    vb = rnd((n, c, h, w), dt, 41)
+    W = rnd((c, c), torch.float32, 42, scale=c ** -0.5)
+    gza, gzb = rnd((n, c, h, w), dt, 43), rnd((n, c, h, w), dt, 44)
+    var, wr = va.clone().requires_grad_(True), W.clone().requires_grad_(True)
+    za, zb = RefModel.coattention(None, var, vb, wr)
+    ((za * gza).sum() + ((zb * gzb).sum() if both else 0)).backward()
+    vag = nhwc(va).to(dt).to(cuda).contiguous().requires_grad_(True)
+    vbg = nhwc(vb).to(dt).to(cuda).contiguous()
+    Wg = W.float().to(cuda).requires_grad_(True)
+    ga, gb = CoattFn.apply(vag, vbg, Wg, (n, h * w))
+    grads = [nhwc(gza).to(dt).to(cuda)]
+    outs = [ga]
+    if both:
+        grads.append(nhwc(gzb).to(dt).to(cuda))
+        outs.append(gb)
+    torch.autograd.backward(outs, grads)
+    torch.cuda.synchronize()
+    tol = {torch.float32: 2e-4, torch.bfloat16: 0.15}[dt]
+    for got, ref in ((ga, za), (gb, zb), (vag.grad, var.grad), (Wg.grad, wr.grad)):
+        if got.dim() == 2 and got.shape[0] == n * h * w:
+            got = nchw(got, n, h, w)
+        got, ref = got.double().cpu(), ref.detach().double()
+        err = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert err <= tol, (err, tol, tuple(ref.shape))
