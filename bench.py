@@ -112,8 +112,15 @@ def main():
         opt.step()
         return loss
 
+    def log(msg):
+        if rank == 0:
+            print("[bench] " + msg, file=sys.stderr, flush=True)
+
     for i in range(args.warmup):
+        t1 = time.perf_counter()
         step(i)
+        torch.cuda.synchronize()
+        log("warmup step %d: %.1f ms" % (i, (time.perf_counter() - t1) * 1e3))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,7 +171,9 @@ def main():
                            "traffic": None, "launches_per_step": n / args.steps,
                            "gemm_time_frac_of_step": kt / dt,
                            "gemm_tflop_per_step": fl / args.steps / 1e12}
+    log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if rank == 0 and args.cpu_baseline and world == 1:
+        log("cpu baseline ...")
         try:
             out["cpu_baseline"] = cpu_baseline(S)
         except Exception as e:  # report, never hide

@@ -39,7 +39,7 @@ _SIGS = {
     "cn_weight_prep": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cn_maxpool_fwd": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cn_maxpool_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
-    "cn_avgpool": (_I, [_I, _P, _L, _I, _I, _I, _F, _P, _P]),
+    "cn_avgpool": (_I, [_I, _P, _L, _I, _I, _I, _F, _P, _P, _P]),
     "cn_bcast_rows": (_I, [_I, _P, _I, _I, _I, _F, _P, _L, _I, _P]),
     "cn_gate_fwd": (_I, [_I, _P, _L, _I, _I, _P, _P, _P, _L, _P, _P]),
     "cn_gate_bwd": (_I, [_I, _P, _L, _P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _P, _P]),

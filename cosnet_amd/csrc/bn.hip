@@ -92,27 +92,46 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
   }
 }
 
-__global__ void bn_stats_finalize(const float* __restrict__ ws, int S, int C, float* mean,
-                                  float* invstd, float* run_mean, float* run_var, float momentum,
-                                  float eps) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double cn = 0, cm = 0, c2 = 0;
-  for (int s = 0; s < S; ++s) {
-    const float* w = ws + ((long long)s * C + c) * 3;
-    double nb = w[0];
-    if (nb == 0) continue;
-    double nn = cn + nb, d = w[1] - cm;
-    cm += d * nb / nn;
-    c2 += w[2] + d * d * cn * nb / nn;
-    cn = nn;
+// block = 64 channels x 16 split-lanes (1024 threads); each lane Chan-merges every 16th split
+// partial, then a 16-way merge through LDS.
+__global__ __launch_bounds__(1024) void bn_stats_finalize(const float* __restrict__ ws, int S, int C,
+                                                          float* mean, float* invstd, float* run_mean,
+                                                          float* run_var, float momentum, float eps) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  float cn = 0.f, cm = 0.f, c2 = 0.f;
+  if (c < C) {
+    for (int s = lane; s < S; s += 16) {
+      const float* w = ws + ((long long)s * C + c) * 3;
+      float nb = w[0], mb = w[1], qb = w[2];
+      if (nb == 0.f) continue;
+      float nn = cn + nb, d = mb - cm, r = nb / nn;
+      cm = fmaf(d, r, cm);
+      c2 += qb + d * d * cn * r;
+      cn = nn;
+    }
   }
-  double var = cn > 0 ? c2 / cn : 0.0;
-  mean[c] = (float)cm;
+  __shared__ float sn[16][64], sm[16][64], s2[16][64];
+  sn[lane][threadIdx.x & 63] = cn;
+  sm[lane][threadIdx.x & 63] = cm;
+  s2[lane][threadIdx.x & 63] = c2;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  double n = 0, m = 0, q = 0;
+  for (int k = 0; k < 16; ++k) {
+    double nb = sn[k][threadIdx.x];
+    if (nb == 0) continue;
+    double nn = n + nb, d = sm[k][threadIdx.x] - m;
+    m += d * nb / nn;
+    q += s2[k][threadIdx.x] + d * d * n * nb / nn;
+    n = nn;
+  }
+  double var = n > 0 ? q / n : 0.0;
+  mean[c] = (float)m;
   invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
   if (run_mean) {
-    double unb = cn > 1 ? c2 / (cn - 1) : var;
-    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * cm);
+    double unb = n > 1 ? q / (n - 1) : var;
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
     run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
   }
 }
@@ -249,18 +268,30 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
   }
 }
 
-__global__ void bn_bwd_finalize(const float* __restrict__ ws, int S, int C, float* sum_dz,
-                                float* sum_dzxh, float* dprelu_c) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0, d = 0;
-  for (int s = 0; s < S; ++s) {
-    const float* w = ws + ((long long)s * C + c) * 3;
-    a += w[0]; b += w[1]; d += w[2];
+__global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict__ ws, int S, int C,
+                                                        float* sum_dz, float* sum_dzxh,
+                                                        float* dprelu_c) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  float a = 0.f, b = 0.f, d = 0.f;
+  if (c < C) {
+    for (int s = lane; s < S; s += 16) {
+      const float* w = ws + ((long long)s * C + c) * 3;
+      a += w[0]; b += w[1]; d += w[2];
+    }
   }
-  sum_dz[c] = (float)a;
-  sum_dzxh[c] = (float)b;
-  if (dprelu_c) dprelu_c[c] = (float)d;
+  __shared__ float ra[16][64], rb[16][64], rd[16][64];
+  ra[lane][threadIdx.x & 63] = a;
+  rb[lane][threadIdx.x & 63] = b;
+  rd[lane][threadIdx.x & 63] = d;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  const int t = threadIdx.x;
+  float A = 0.f, Bs = 0.f, D = 0.f;
+  for (int k = 0; k < 16; ++k) { A += ra[k][t]; Bs += rb[k][t]; D += rd[k][t]; }
+  sum_dz[c] = A;
+  sum_dzxh[c] = Bs;
+  if (dprelu_c) dprelu_c[c] = D;
 }
 
 // dx = gamma*invstd*(dz - sum_dz/P - xhat*sum_dzxh/P);  dres = dz (optional)
@@ -317,11 +348,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   }
 }
 
-template <class T> int grid_rows(int P, int C, int* gx) {
+// Row blocks for a launch: ~`blocks` blocks in total, each thread walking >= min_rows rows.
+// Reductions (stats, backward sums) use min_rows 8 so the split count stays small for the
+// finalize pass; pure streaming passes (apply) use 2 for more parallelism.
+template <class T> int grid_rows(int P, int C, int* gx, int min_rows = 8, int blocks = 1024) {
   Layout L = layout_of<T>(C);
   *gx = (L.CPR + L.CB - 1) / L.CB;
-  int want = (2048 + *gx - 1) / *gx;             // ~2048 blocks
-  int maxy = (P + L.RPB - 1) / L.RPB;
+  int want = (blocks + *gx - 1) / *gx;
+  int maxy = (P + min_rows * L.RPB - 1) / (min_rows * L.RPB);
   int gy = want < maxy ? want : maxy;
   return gy < 1 ? 1 : gy;
 }
@@ -352,7 +386,7 @@ extern "C" int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int C
     hipLaunchKernelGGL(bn_stats_partial<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C, ws);
   }
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 255) / 256), dim3(256), 0, st, ws, gy, C, mean,
+  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, ws, gy, C, mean,
                      invstd, run_mean, run_var, momentum, eps);
   CN_CHECK_LAUNCH();
   return 0;
@@ -373,12 +407,12 @@ extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C
                            long long ldy, hipStream_t st) {
   int gx, gy;
   if (dtype == DT_BF16) {
-    gy = grid_rows<bf16>(P, C, &gx);
+    gy = grid_rows<bf16>(P, C, &gx, 2, 2048);
     hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
                        rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy);
   } else {
-    gy = grid_rows<float>(P, C, &gx);
+    gy = grid_rows<float>(P, C, &gx, 2, 2048);
     hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
                        rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy);
@@ -406,9 +440,10 @@ extern "C" int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy
                        beta, act, prelu, ws);
   }
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
   CN_CHECK_LAUNCH();
   if (!dx) return 0;
+  gy = dtype == DT_BF16 ? grid_rows<bf16>(P, C, &gx, 2, 2048) : grid_rows<float>(P, C, &gx, 2, 2048);
   if (dtype == DT_BF16) {
     hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
                        (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,

@@ -125,20 +125,22 @@ __global__ void maxpool_bwd_k(const T* __restrict__ dy, const unsigned char* __r
 }
 
 // ---- global average pool over HW per image: T [N*HW][C] (ld) -> T [N][C] --------------
+// grid (ceil(C/V/64), N, RS): block = 64 chunks x 4 row groups; fp32 partials -> ws [N][C]
 template <class T>
-__global__ void avgpool_k(const T* __restrict__ x, long long ld, int HW, int C, float scale,
-                          T* __restrict__ y) {
-  // grid (C/VEC chunks / 64, N); block 256 = 64 chunks x 4 row groups
+__global__ __launch_bounds__(256) void avgpool_partial_k(const T* __restrict__ x, long long ld, int HW,
+                                                         int C, float* __restrict__ ws) {
   constexpr int V = VecOf<T>::N;
-  int cc = blockIdx.x * 64 + (threadIdx.x & 63);
-  int rg = threadIdx.x >> 6;
-  int n = blockIdx.y;
+  const int cc = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int n = blockIdx.y;
+  const int per = (HW + gridDim.z - 1) / gridDim.z;
+  const int r0 = blockIdx.z * per, r1 = min(HW, r0 + per);
   __shared__ float red[4][64][8];
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
   if (cc * V < C) {
-    for (int r = rg; r < HW; r += 4) {
+    for (int r = r0 + rg; r < r1; r += 4) {
       float f[V];
       ldv(x + ((long long)n * HW + r) * ld + cc * V, f);
 #pragma unroll
@@ -149,13 +151,18 @@ __global__ void avgpool_k(const T* __restrict__ x, long long ld, int HW, int C, 
   for (int v = 0; v < V; ++v) red[rg][threadIdx.x & 63][v] = acc[v];
   __syncthreads();
   if (rg == 0 && cc * V < C) {
-    float o[V];
 #pragma unroll
     for (int v = 0; v < V; ++v)
-      o[v] = (red[0][threadIdx.x][v] + red[1][threadIdx.x][v] + red[2][threadIdx.x][v] +
-              red[3][threadIdx.x][v]) * scale;
-    stv(y + (long long)n * C + cc * V, o);
+      atomicAdd(ws + (long long)n * C + cc * V + v, red[0][threadIdx.x][v] + red[1][threadIdx.x][v] +
+                                                        red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
   }
+}
+
+template <class T>
+__global__ void scale_cast_k(const float* __restrict__ ws, long long n, float scale, T* __restrict__ y) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = fromf<T>(ws[i] * scale);
 }
 
 // broadcast T [N][C] over HW rows into dst (ld); scale applied (1 for fwd, 1/HW for avgpool bwd)
@@ -215,39 +222,61 @@ __global__ void gate_fwd_k(const T* __restrict__ z, long long ldz, int P, int C,
 }
 
 // dz = dout*m + (sum_c dout*z) * m(1-m) * g ;  dg += sum_p (.)*z ; dgb += sum_p (.)
+// one wave per row, rows grid-strided; dg / dgb reduced per block before one atomic each.
 template <class T>
-__global__ void gate_bwd_k(const T* __restrict__ z, long long ldz, const T* __restrict__ dout,
-                           long long lddo, const float* __restrict__ mask, int P, int C,
-                           const float* __restrict__ g, int through_mask, T* __restrict__ dz,
-                           long long lddz, float* __restrict__ dg, float* __restrict__ dgb) {
+__global__ __launch_bounds__(256) void gate_bwd_k(const T* __restrict__ z, long long ldz,
+                                                  const T* __restrict__ dout, long long lddo,
+                                                  const float* __restrict__ mask, int P, int C,
+                                                  const float* __restrict__ g, int through_mask,
+                                                  T* __restrict__ dz, long long lddz,
+                                                  float* __restrict__ dg, float* __restrict__ dgb) {
   constexpr int V = VecOf<T>::N;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int CPR = C / V;
-  if (row >= P) return;
-  float dm = 0.f;
-  for (int cc = through_mask ? lane : CPR; cc < CPR; cc += 64) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int CPR = C / V;  // <= 64 (checked by the launcher)
+  const bool on = lane < CPR;
+  float gv[V], acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) { gv[v] = on ? g[lane * V + v] : 0.f; acc[v] = 0.f; }
+  float accb = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < P; row += gridDim.x * 4) {
     float f[V], d[V];
-    ldv(z + (long long)row * ldz + cc * V, f);
-    ldv(dout + (long long)row * lddo + cc * V, d);
+    if (on) {
+      ldv(z + (long long)row * ldz + lane * V, f);
+      ldv(dout + (long long)row * lddo + lane * V, d);
+    } else {
 #pragma unroll
-    for (int v = 0; v < V; ++v) dm = fmaf(f[v], d[v], dm);
-  }
-  dm = warp_sum(dm);
-  const float m = mask[row];
-  const float dpre = dm * m * (1.f - m);
-  if (lane == 0 && dgb) atomicAdd(dgb, dpre);
-  for (int cc = lane; cc < CPR; cc += 64) {
-    float f[V], d[V], o[V];
-    ldv(z + (long long)row * ldz + cc * V, f);
-    ldv(dout + (long long)row * lddo + cc * V, d);
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      o[v] = d[v] * m + dpre * g[cc * V + v];
-      if (dg) atomicAdd(dg + cc * V + v, dpre * f[v]);
+      for (int v = 0; v < V; ++v) f[v] = d[v] = 0.f;
     }
-    stv(dz + (long long)row * lddz + cc * V, o);
+    float dm = 0.f;
+    if (through_mask) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) dm = fmaf(f[v], d[v], dm);
+      dm = warp_sum(dm);
+    }
+    const float m = mask[row];
+    const float dpre = dm * m * (1.f - m);
+    accb += dpre;
+    if (on) {
+      float o[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        o[v] = d[v] * m + dpre * gv[v];
+        acc[v] = fmaf(dpre, f[v], acc[v]);
+      }
+      stv(dz + (long long)row * lddz + lane * V, o);
+    }
   }
+  if (!dg) return;
+  __shared__ float red[4][64][8];
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[wave][lane][v] = acc[v];
+  __syncthreads();
+  if (wave == 0 && on) {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      atomicAdd(dg + lane * V + v, red[0][lane][v] + red[1][lane][v] + red[2][lane][v] + red[3][lane][v]);
+  }
+  if (dgb && lane == 0) atomicAdd(dgb, accb);
 }
 
 // ---- decoder head: zr = relu(a [+ b]) (stored if zout), logit = zr . w + bias ---------------
@@ -284,27 +313,42 @@ __global__ void head_fwd_k(const T* __restrict__ a, long long lda, const T* __re
 }
 
 template <class T>
-__global__ void head_bwd_k(const T* __restrict__ z, long long ldz, const float* __restrict__ dlogit,
-                           int P, int C, int relu, const float* __restrict__ w,
-                           T* __restrict__ dz, long long lddz, float* __restrict__ dw,
-                           float* __restrict__ db) {
+__global__ __launch_bounds__(256) void head_bwd_k(const T* __restrict__ z, long long ldz,
+                                                  const float* __restrict__ dlogit, int P, int C,
+                                                  int relu, const float* __restrict__ w,
+                                                  T* __restrict__ dz, long long lddz,
+                                                  float* __restrict__ dw, float* __restrict__ db) {
   constexpr int V = VecOf<T>::N;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= P) return;
-  const int CPR = C / V;
-  const float dl = dlogit[row];
-  if (lane == 0 && db) atomicAdd(db, dl);
-  for (int cc = lane; cc < CPR; cc += 64) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int CPR = C / V;  // <= 64 (checked by the launcher)
+  const bool on = lane < CPR;
+  float wv[V], acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) { wv[v] = on ? w[lane * V + v] : 0.f; acc[v] = 0.f; }
+  float accb = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < P; row += gridDim.x * 4) {
+    const float dl = dlogit[row];
+    accb += dl;
+    if (!on) continue;
     float f[V], o[V];
-    ldv(z + (long long)row * ldz + cc * V, f);
+    ldv(z + (long long)row * ldz + lane * V, f);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      o[v] = (!relu || f[v] > 0.f) ? dl * w[cc * V + v] : 0.f;
-      if (dw) atomicAdd(dw + cc * V + v, dl * f[v]);
+      o[v] = (!relu || f[v] > 0.f) ? dl * wv[v] : 0.f;
+      acc[v] = fmaf(dl, f[v], acc[v]);
     }
-    if (dz) stv(dz + (long long)row * lddz + cc * V, o);
+    if (dz) stv(dz + (long long)row * lddz + lane * V, o);
   }
+  __shared__ float red[4][64][8];
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[wave][lane][v] = acc[v];
+  __syncthreads();
+  if (dw && wave == 0 && on) {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      atomicAdd(dw + lane * V + v, red[0][lane][v] + red[1][lane][v] + red[2][lane][v] + red[3][lane][v]);
+  }
+  if (db && lane == 0) atomicAdd(db, accb);
 }
 
 // ---- bilinear upsample (align_corners=False, torch semantics) + sigmoid ----------------
@@ -568,13 +612,24 @@ extern "C" int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* ar
 }
 
 extern "C" int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C,
-                          float scale, void* y, hipStream_t st) {
+                          float scale, void* y, float* ws, hipStream_t st) {
   int V = dtype == DT_BF16 ? 8 : 4;
-  dim3 grid((C / V + 63) / 64, N);
+  if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)N * C, st) != hipSuccess) return CN_ERR_HIP;
+  int gx = (C / V + 63) / 64;
+  int rs = (HW + 255) / 256;
+  if (rs * gx * N > 1024) rs = 1024 / (gx * N);
+  if (rs < 1) rs = 1;
+  dim3 grid(gx, N, rs);
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(avgpool_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, HW, C, scale, (bf16*)y);
+    hipLaunchKernelGGL(avgpool_partial_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, HW, C, ws);
   else
-    hipLaunchKernelGGL(avgpool_k<float>, grid, dim3(256), 0, st, (const float*)x, ld, HW, C, scale, (float*)y);
+    hipLaunchKernelGGL(avgpool_partial_k<float>, grid, dim3(256), 0, st, (const float*)x, ld, HW, C, ws);
+  CN_CHECK_LAUNCH();
+  long long n = (long long)N * C;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(scale_cast_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, ws, n, scale, (bf16*)y);
+  else
+    hipLaunchKernelGGL(scale_cast_k<float>, dim3(nblocks(n)), dim3(256), 0, st, ws, n, scale, (float*)y);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -604,7 +659,8 @@ extern "C" int cn_gate_fwd(int dtype, const void* z, long long ldz, int P, int C
 extern "C" int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
                            const float* mask, int P, int C, const float* g, int through_mask,
                            void* dz, long long lddz, float* dg, float* dgb, hipStream_t st) {
-  dim3 grid((P + 3) / 4);
+  if (C / (dtype == DT_BF16 ? 8 : 4) > 64) return CN_ERR_UNSUPPORTED;
+  dim3 grid(nblocks(P, 4 * 16));
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(gate_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, (const bf16*)dout, lddo, mask, P, C, g, through_mask, (bf16*)dz, lddz, dg, dgb);
   else
@@ -628,7 +684,8 @@ extern "C" int cn_head_fwd(int dtype, const void* a, long long lda, const void* 
 extern "C" int cn_head_bwd(int dtype, const void* z, long long ldz, const float* dlogit, int P, int C,
                            int relu, const float* w, void* dz, long long lddz, float* dw, float* db,
                            hipStream_t st) {
-  dim3 grid((P + 3) / 4);
+  if (C / (dtype == DT_BF16 ? 8 : 4) > 64) return CN_ERR_UNSUPPORTED;
+  dim3 grid(nblocks(P, 4 * 16));
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(head_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, dlogit, P, C, relu, w, (bf16*)dz, lddz, dw, db);
   else

@@ -312,14 +312,32 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  // Epilogue: lane holds C[4g + r][l & 15] of each 16x16 block.
+  // Epilogue: stage alpha*acc (fp32) through LDS as [BM/2][BN+4] one wave-row half at a time,
+  // then every thread writes 8 consecutive columns of a row (16-B bf16 / 2x16-B fp32 stores,
+  // or 8 contiguous atomics).  Lane holds C[4g + r][l & 15] of each 16x16 block.
+  constexpr int LDC = BN + 4;
+  constexpr int HR = BM / 2;
+  static_assert(HR * LDC * 4 <= 2 * STAGE, "epilogue staging must fit in the LDS image");
+  float* cs = (float*)smem;
   CT* Cb = (CT*)p.C + (long long)batch * p.c_bs;
-  const int g = lane >> 4;
+  constexpr int GPR = BN / 8;            // 8-column groups per row
+  constexpr int RPP = NT / GPR;          // rows per pass
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
+      const int g = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < RM; ++i) {
+      for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int row = m0 + wm * (BM / 2) + i * 16 + 4 * g + r;
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[(i * 16 + 4 * g + r) * LDC + wn * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r] * p.alpha;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int rr = tid / GPR; rr < HR; rr += RPP) {
+      const int row = m0 + half * HR + rr;
       if (row >= p.M) continue;
       long long drow = row;
       if (p.row_map == 1) {  // stride-2 dgrad scatter: row over (n, oy, ox) -> (n, 2oy, 2ox)
@@ -328,15 +346,47 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
         fdivmod(rem, p.rm_div_OW, oy, ox);
         drow = ((long long)im * p.rm_H + 2 * oy) * p.rm_W + 2 * ox;
       }
+      const int c0 = (tid % GPR) * 8;
+      const int col = n0 + c0;
+      if (col >= p.N) continue;
+      float v[8];
+      *(f32x4*)&v[0] = *(const f32x4*)&cs[rr * LDC + c0];
+      *(f32x4*)&v[4] = *(const f32x4*)&cs[rr * LDC + c0 + 4];
+      CT* dst = Cb + drow * p.ldc + col;
+      const bool full = col + 8 <= p.N && ((uintptr_t)dst % 16 == 0);
+      if (p.bias) {
 #pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-        if (col >= p.N) continue;
-        float v = acc[i][j][r] * p.alpha;
-        if (p.bias) v += p.bias[col];
-        store_c<CT>(Cb + drow * p.ldc + col, v, p.c_mode);
+        for (int e = 0; e < 8; ++e) v[e] += (col + e < p.N) ? p.bias[col + e] : 0.f;
+      }
+      if (p.c_mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col + e < p.N) store_c<CT>(dst + e, v[e], 1);
+      } else if (full) {
+        if constexpr (sizeof(CT) == 2) {
+          if (p.c_mode == 2) {
+            float q[8];
+            Chunk<bf16>::unpack(*(const u32x4*)dst, q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += q[e];
+          }
+          *(u32x4*)dst = Chunk<bf16>::pack(v);
+        } else {
+          if (p.c_mode == 2) {
+            f32x4 q0 = *(const f32x4*)dst, q1 = *(const f32x4*)(dst + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[e] += q0[e]; v[4 + e] += q1[e]; }
+          }
+          *(f32x4*)dst = *(f32x4*)&v[0];
+          *(f32x4*)(dst + 4) = *(f32x4*)&v[4];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col + e < p.N) store_c<CT>(dst + e, v[e], p.c_mode);
       }
     }
+    __syncthreads();
   }
 }
 
@@ -353,7 +403,9 @@ static int launch_t(const GemmArgs& a, int batch, hipStream_t st) {
 
 template <class T, class CT, int LA, int LB>
 static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
-  if (a.N <= 64) return launch_t<T, CT, 128, 64, LA, LB>(a, batch, st);
+  // 128x128 when it yields >= 1.5 waves of blocks over the 256 CUs, else 128x64
+  long long t128 = (long long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch * a.nsplit;
+  if (a.N <= 64 || t128 < 384) return launch_t<T, CT, 128, 64, LA, LB>(a, batch, st);
   return launch_t<T, CT, 128, 128, LA, LB>(a, batch, st);
 }
 

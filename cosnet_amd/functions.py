@@ -159,8 +159,9 @@ class ASPPFn(F):
         dev = x.device
         cat = torch.empty((P, 2560), dtype=dt, device=dev)
         pool = torch.empty((n, 2048), dtype=dt, device=dev)
+        apws = torch.empty((n * 2048,), dtype=torch.float32, device=dev)
         nv.call("cn_avgpool", ops.dtc(x), x.data_ptr(), ops.ld(x), n, hw, 2048, 1.0 / hw,
-                pool.data_ptr(), nv.stream())
+                pool.data_ptr(), apws.data_ptr(), nv.stream())
         wcf, wct = WCACHE.get(wc, dt)
         cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=bc)
         stp = bn_stats(cp, mod.bn_x, tr)
@@ -219,8 +220,9 @@ class ASPPFn(F):
             grads.append((dwi, dbias, dgi, dbi))
         # image-pool branch: sum over HW of its cat slice
         dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
+        apws = torch.empty((n * 512,), dtype=torch.float32, device=dout.device)
         nv.call("cn_avgpool", ops.dtc(dcat), dcat.data_ptr(), ops.ld(dcat), n, hw, 512, 1.0,
-                dyp.data_ptr(), nv.stream())
+                dyp.data_ptr(), apws.data_ptr(), nv.stream())
         dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp, mod.bn_x, act=1)
         dwc = conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1)
         dbc = ops.colsum(dcp)

@@ -97,7 +97,7 @@ int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* argmax, int N
                    int C, int OH, int OW, int k, int s, int pad, void* dx, hipStream_t stream);
 /* AdaptiveAvgPool2d(1) + 1x1 upsample broadcast: deeplab/deeplabv3_encoder.py:57-61 */
 int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C, float scale, void* y,
-               hipStream_t stream);
+               float* ws /* N*C floats */, hipStream_t stream);
 int cn_bcast_rows(int dtype, const void* src, int N, int HW, int C, float scale, void* dst,
                   long long ld, int accumulate, hipStream_t stream);
 /* gate: rgbd_segmentation_RAA.py:177-184 (RGB, no bias), :228-235 (depth, bias) */
