@@ -33,6 +33,14 @@ __device__ __forceinline__ int mc_swz(int k, int granules_per_row) {
   return (granules_per_row >= 32 ? h : (h & 3)) << 2;
 }
 
+// 16 zero bytes in global memory: out-of-bounds lanes of an LDS-DMA fill read from here.
+__device__ __attribute__((aligned(16))) unsigned g_zero16[4];
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
 // -------------------------------------------------------------------------------------
 // Operand loader.  ROWS = BM (A) or BN (B).  Fills `ROWS/32` 16-byte chunks per thread.
 // -------------------------------------------------------------------------------------
@@ -128,6 +136,66 @@ template <class T, int ROWS, int KIND> struct Loader {
         bool ok = colok && p < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
         long long pix = ((long long)im * g.H + y) * g.W + x;
         v[i] = ok ? *(const u32x4*)(base + pix * ld + ci) : zero;
+      }
+    }
+  }
+
+  // LDS-DMA fill (global_load_lds_dwordx4): chunk q = tid + 256 i lands at byte 16 q of the
+  // tile (lane-linear per wave instruction); the XOR swizzle moves to the SOURCE chunk so the
+  // image is identical to store()'s.  Out-of-bounds chunks read the zero page.
+  __device__ __forceinline__ void issue(int k0, int origin, int tid, char* lds) const {
+    const void* zp = (const void*)g_zero16;
+    char* wbase = lds + (tid & ~63) * 16;
+    if (!MC) {
+      const int pos = tid & 7;
+      const int c = pos ^ ((tid >> 3) & 7);  // row & 7 == (tid >> 3) & 7 for every i
+      const int k = k0 + c * VEC;
+      if (KIND == L_KC_DENSE) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          int row = origin + (tid >> 3) + 32 * i;
+          bool ok = row < lim && k < klim;
+          glds16(ok ? (const void*)(base + (long long)row * ld + k) : zp, wbase + i * 4096);
+        }
+      } else {  // L_KC_CONV
+        int tap, cc, r, ss;
+        fdivmod(k < klim ? k : 0, g.div_C, tap, cc);
+        fdivmod(tap, g.div_KW, r, ss);
+        int oy = r * g.step_y, ox = ss * g.step_x;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          int y = by[i] + oy, x = bx[i] + ox;
+          bool ok = img[i] >= 0 && k < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+          long long pix = ((long long)img[i] * g.H + y) * g.W + x;
+          glds16(ok ? (const void*)(base + pix * ld + cc) : zp, wbase + i * 4096);
+        }
+      }
+    } else {
+      constexpr int RB = ROWS * (int)sizeof(T);
+      const int pos = tid % CPR;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int krl = tid / CPR + KROW_STEP * i;          // k-row within the tile
+        const int cchunk = (sizeof(T) == 2) ? (pos ^ (mc_swz(krl, RB / 8) >> 1)) : pos;
+        const int kr = k0 + krl;
+        const int col = origin + cchunk * VEC;
+        const void* src = zp;
+        if (KIND == L_MC_DENSE) {
+          if (kr < klim && col < lim) src = base + (long long)kr * ld + col;
+        } else {  // L_MC_CONV: n = (tap, ci) fixed per chunk column
+          int nn = col < lim ? col : 0;
+          int tap, cic, r, ss;
+          fdivmod(nn, g.div_C, tap, cic);
+          fdivmod(tap, g.div_KW, r, ss);
+          int pp = kr < klim ? kr : 0;
+          int im, rem, oy, ox;
+          fdivmod(pp, g.div_OHW, im, rem);
+          fdivmod(rem, g.div_OW, oy, ox);
+          int y = oy * g.st + r * g.step_y + g.off_y, x = ox * g.st + ss * g.step_x + g.off_x;
+          if (col < lim && kr < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
+            src = base + (((long long)im * g.H + y) * g.W + x) * ld + cic;
+        }
+        glds16(src, wbase + i * 4096);
       }
     }
   }
@@ -244,21 +312,19 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[BM / 32], rb[BN / 32];
   if (nt > 0) {
-    la.load(kbeg, m0, tid, ra);
-    lb.load(kbeg, n0, tid, rb);
-    la.store(smem, tid, ra);
-    lb.store(smem + ABYTES, tid, rb);
+    la.issue(kbeg, m0, tid, smem);
+    lb.issue(kbeg, n0, tid, smem + ABYTES);
   }
-  __syncthreads();
+  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed for every wave
 
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nt;
-    if (more) {
-      la.load(kbeg + (kt + 1) * BK, m0, tid, ra);
-      lb.load(kbeg + (kt + 1) * BK, n0, tid, rb);
+    if (more) {  // DMA the next tile into the other buffer while this one is consumed
+      char* nxt = smem + (cur ^ 1) * STAGE;
+      la.issue(kbeg + (kt + 1) * BK, m0, tid, nxt);
+      lb.issue(kbeg + (kt + 1) * BK, n0, tid, nxt + ABYTES);
     }
     const char* As = smem + cur * STAGE;
     const char* Bs = As + ABYTES;
@@ -304,12 +370,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
       }
     }
-    if (more) {
-      char* nxt = smem + (cur ^ 1) * STAGE;
-      la.store(nxt, tid, ra);
-      lb.store(nxt + ABYTES, tid, rb);
-    }
-    __syncthreads();
+    __syncthreads();  // drains this wave's DMA (vmcnt(0)) and orders it for all readers
   }
 
   // Epilogue: stage alpha*acc (fp32) through LDS as [BM/2][BN+4] one wave-row half at a time,
