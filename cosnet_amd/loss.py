@@ -11,18 +11,25 @@ import torch.distributed as dist
 from . import functions as fn
 
 
-def positive_ratio(label, group=None):
-    cnt = fn.count_positive(label)
-    n, _, h, w = label.shape
-    total = torch.tensor([n * h * w], dtype=torch.int64, device=label.device)
+def global_ratio(cnt, total, group=None):
+    """N*H*W / #(gt >= 0.5) over the global batch: (cnt, total) int64 [1] tensors are
+    summed over ranks when a process group is up.  None if there is no positive pixel
+    (train.py:185-187 falls back to an unweighted BCE)."""
     if dist.is_available() and dist.is_initialized():
-        both = torch.cat([cnt, total])
+        both = torch.cat([cnt.reshape(1), total.reshape(1)])
         dist.all_reduce(both, group=group)
         cnt, total = both[:1], both[1:]
     npos = int(cnt.item())
     if npos == 0:
         return None
     return float(int(total.item())) / npos
+
+
+def positive_ratio(label, group=None):
+    cnt = fn.count_positive(label)
+    n, _, h, w = label.shape
+    total = torch.tensor([n * h * w], dtype=torch.int64, device=label.device)
+    return global_ratio(cnt, total, group)
 
 
 def calc_loss_BCE(pred, label, ratio="auto"):
