@@ -12,6 +12,8 @@
 
 namespace {
 
+constexpr int UNR = 4;  // rows in flight per thread in the streaming loops
+
 struct Layout {
   int CPR, CB, RPB;
 };
@@ -44,20 +46,27 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
 #pragma unroll
   for (int v = 0; v < V; ++v) { sh[v] = 0.f; s[v] = 0.f; ss[v] = 0.f; }
   if (act) {
-    for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
-      float f[V];
-      ld_chunk(x + (long long)r * ld + chunk * V, f);
+    const int step = gridDim.y * L.RPB;
+    for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
+      float f[UNR][V];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)  // UNR independent 16-B loads in flight per thread
+        if (r0 + u * step < P) ld_chunk(x + (long long)(r0 + u * step) * ld + chunk * V, f[u]);
       if (n == 0) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) sh[v] = f[v];
+        for (int v = 0; v < V; ++v) sh[v] = f[0][v];
       }
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        float d = f[v] - sh[v];
-        s[v] += d;
-        ss[v] = fmaf(d, d, ss[v]);
+      for (int u = 0; u < UNR; ++u) {
+        if (r0 + u * step >= P) break;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          float d = f[u][v] - sh[v];
+          s[v] += d;
+          ss[v] = fmaf(d, d, ss[v]);
+        }
+        ++n;
       }
-      ++n;
     }
   }
   // per-thread (mean, M2)
@@ -173,31 +182,32 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
     }
   }
   const float a = (act == 2) ? prelu[0] : 0.f;
-  for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
-    float f[V];
-    ld_chunk(x + (long long)r * ldx + chunk * V, f);
+  const int step = gridDim.y * L.RPB;
+  for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
+    float f[UNR][V], q[UNR][V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) f[v] = fmaf(f[v], sc[v], sf[v]);
-    if (res) {
-      float q[V];
-      ld_chunk(res + (long long)r * ldr + chunk * V, q);
-#pragma unroll
-      for (int v = 0; v < V; ++v) f[v] += q[v];
+    for (int u = 0; u < UNR; ++u) {
+      const int r = r0 + u * step;
+      if (r >= P) break;
+      ld_chunk(x + (long long)r * ldx + chunk * V, f[u]);
+      if (res) ld_chunk(res + (long long)r * ldr + chunk * V, q[u]);
+      if (xr) ld_chunk(xr + (long long)r * ldxr + chunk * V, q[u]);
     }
-    if (xr) {
-      float q[V];
-      ld_chunk(xr + (long long)r * ldxr + chunk * V, q);
 #pragma unroll
-      for (int v = 0; v < V; ++v) f[v] += fmaf(q[v], rsc[v], rsf[v]);
+    for (int u = 0; u < UNR; ++u) {
+      const int r = r0 + u * step;
+      if (r >= P) break;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float t = fmaf(f[u][v], sc[v], sf[v]);
+        if (res) t += q[u][v];
+        if (xr) t += fmaf(q[u][v], rsc[v], rsf[v]);
+        if (act == 1) t = fmaxf(t, 0.f);
+        else if (act == 2) t = t > 0.f ? t : a * t;
+        f[u][v] = t;
+      }
+      st_chunk(y + (long long)r * ldy + chunk * V, f[u]);
     }
-    if (act == 1) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) f[v] = fmaxf(f[v], 0.f);
-    } else if (act == 2) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) f[v] = f[v] > 0.f ? f[v] : a * f[v];
-    }
-    st_chunk(y + (long long)r * ldy + chunk * V, f);
   }
 }
 
@@ -226,25 +236,31 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
   }
   const float a = (act == 2) ? prelu[0] : 0.f;
   if (on) {
-    for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
-      float xf[V], d[V];
-      ld_chunk(x + (long long)r * ldx + chunk * V, xf);
-      ld_chunk(dy + (long long)r * lddy + chunk * V, d);
-      if (act == 1) {
-        float yf[V];
-        ld_chunk(y + (long long)r * ldy + chunk * V, yf);
+    const int step = gridDim.y * L.RPB;
+    for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
+      float xf[UNR][V], d[UNR][V], yf[UNR][V];
 #pragma unroll
-        for (int v = 0; v < V; ++v) d[v] = yf[v] > 0.f ? d[v] : 0.f;
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * step;
+        if (r >= P) break;
+        ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
+        ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
+        if (act == 1) ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
       }
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        float xh = (xf[v] - mu[v]) * is[v];
-        if (act == 2) {
-          float pre = fmaf(xh, g[v], b[v]);
-          if (pre <= 0.f) { s3[v] = fmaf(d[v], pre, s3[v]); d[v] *= a; }
+      for (int u = 0; u < UNR; ++u) {
+        if (r0 + u * step >= P) break;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
+          float xh = (xf[u][v] - mu[v]) * is[v];
+          if (act == 2) {
+            float pre = fmaf(xh, g[v], b[v]);
+            if (pre <= 0.f) { s3[v] = fmaf(dd, pre, s3[v]); dd *= a; }
+          }
+          s1[v] += dd;
+          s2[v] = fmaf(dd, xh, s2[v]);
         }
-        s1[v] += d[v];
-        s2[v] = fmaf(d[v], xh, s2[v]);
       }
     }
   }
@@ -323,28 +339,36 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
     m2[v] = sum_dzxh[c] * invP;
   }
   const float a = (act == 2) ? prelu[0] : 0.f;
-  for (int r = blockIdx.y * L.RPB + ty; r < P; r += gridDim.y * L.RPB) {
-    float xf[V], d[V];
-    ld_chunk(x + (long long)r * ldx + chunk * V, xf);
-    ld_chunk(dy + (long long)r * lddy + chunk * V, d);
-    if (act == 1) {
-      float yf[V];
-      ld_chunk(y + (long long)r * ldy + chunk * V, yf);
+  const int step = gridDim.y * L.RPB;
+  for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
+    float xf[UNR][V], d[UNR][V], yf[UNR][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) d[v] = yf[v] > 0.f ? d[v] : 0.f;
+    for (int u = 0; u < UNR; ++u) {
+      const int r = r0 + u * step;
+      if (r >= P) break;
+      ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
+      ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
+      if (act == 1) ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
     }
-    float o[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float xh = (xf[v] - mu[v]) * is[v];
-      if (act == 2) {
-        float pre = fmaf(xh, g[v], b[v]);
-        if (pre <= 0.f) d[v] *= a;
+    for (int u = 0; u < UNR; ++u) {
+      const int r = r0 + u * step;
+      if (r >= P) break;
+      float o[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
+        float xh = (xf[u][v] - mu[v]) * is[v];
+        if (act == 2) {
+          float pre = fmaf(xh, g[v], b[v]);
+          if (pre <= 0.f) dd *= a;
+        }
+        o[v] = k1[v] * (dd - m1[v] - xh * m2[v]);
+        d[u][v] = dd;
       }
-      o[v] = k1[v] * (d[v] - m1[v] - xh * m2[v]);
+      st_chunk(dx + (long long)r * lddx + chunk * V, o);
+      if (dres) st_chunk(dres + (long long)r * lddres + chunk * V, d[u]);
     }
-    st_chunk(dx + (long long)r * lddx + chunk * V, o);
-    if (dres) st_chunk(dres + (long long)r * lddres + chunk * V, d);
   }
 }
 
@@ -407,12 +431,12 @@ extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C
                            long long ldy, hipStream_t st) {
   int gx, gy;
   if (dtype == DT_BF16) {
-    gy = grid_rows<bf16>(P, C, &gx, 2, 2048);
+    gy = grid_rows<bf16>(P, C, &gx, UNR, 2048);
     hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
                        rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy);
   } else {
-    gy = grid_rows<float>(P, C, &gx, 2, 2048);
+    gy = grid_rows<float>(P, C, &gx, UNR, 2048);
     hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
                        rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy);
@@ -443,7 +467,7 @@ extern "C" int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
   CN_CHECK_LAUNCH();
   if (!dx) return 0;
-  gy = dtype == DT_BF16 ? grid_rows<bf16>(P, C, &gx, 2, 2048) : grid_rows<float>(P, C, &gx, 2, 2048);
+  gy = dtype == DT_BF16 ? grid_rows<bf16>(P, C, &gx, UNR, 2048) : grid_rows<float>(P, C, &gx, UNR, 2048);
   if (dtype == DT_BF16) {
     hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
                        (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,

@@ -1,0 +1,65 @@
+"""N-reference inference of test.py (:287-305) and its evaluation (:307-344).
+
+The reference re-encodes the target frame once per reference frame and averages x1 over the
+N forwards.  In eval mode every op is per-sample (BN uses running statistics), so encoding
+the target once, the N search frames as one batch, and running the co-attention head on the
+N-way stack gives the same average (6e-8 in fp32) with 1 + N instead of 2N
+encoder passes.
+"""
+import torch
+
+from . import _native as nv
+from . import ops
+
+
+@torch.no_grad()
+def multi_reference_x1(model, target, target_depth, searches, search_depths):
+    """target [1,3,H,W], target_depth [1,1,H,W], searches [N,3,H,W], search_depths [N,1,H,W]
+    (fp32 NCHW on the GPU) -> mean over the N references of x1, [1,1,H,W] fp32."""
+    if model.training:
+        raise RuntimeError("multi-reference inference runs in eval mode (test.py:230)")
+    model._set_dtype()
+    target, target_depth, searches, search_depths = map(
+        model._prep, (target, target_depth, searches, search_depths))
+    n = searches.shape[0]
+    input_size = tuple(target.shape[2:])
+    va, geo1 = model.encoder.features_nhwc(target)
+    da, _ = model.depth_encoder.features_nhwc(target_depth)
+    vb, geo = model.encoder.features_nhwc(searches)
+    db, _ = model.depth_encoder.features_nhwc(search_depths)
+    p1 = va.shape[0]
+    va_n = torch.empty((n * p1, va.shape[1]), dtype=va.dtype, device=va.device)
+    da_n = torch.empty_like(va_n)
+    for i in range(n):  # stack the target features N times (one copy kernel each)
+        ops.cast_copy(va, va_n[i * p1:(i + 1) * p1])
+        ops.cast_copy(da, da_n[i * p1:(i + 1) * p1])
+    x1, _ = model.head_nhwc(va_n, vb, da_n, db, geo, input_size)
+    out = torch.empty((1, 1) + input_size, dtype=torch.float32, device=x1.device)
+    hw = input_size[0] * input_size[1]
+    # mean over the N outputs: a [N][HW] -> [1][HW] column reduction, then 1/N scaling
+    acc = torch.zeros((hw,), dtype=torch.float32, device=x1.device)
+    nv.call("cn_colsum", nv.DT_F32, x1.data_ptr(), hw, n, hw, acc.data_ptr(), nv.stream())
+    nv.call("cn_cast2d", nv.DT_F32, nv.DT_F32, acc.data_ptr(), hw, 1, hw, out.data_ptr(), hw, 0,
+            nv.stream())
+    out.mul_(1.0 / n)
+    return out
+
+
+@torch.no_grad()
+def resize_linear(x, out_hw):
+    """cv2.resize(..., INTER_LINEAR) of a float map (half-pixel centres, no antialias), which is
+    bilinear with align_corners=False: the upsample kernel without the sigmoid."""
+    n, c, h, w = x.shape
+    assert c == 1
+    H, W = out_hw
+    if (H, W) == (h, w):
+        return x
+    out = torch.empty((n, 1, H, W), dtype=torch.float32, device=x.device)
+    src = x.contiguous()
+    nv.call("cn_upsample_sigmoid", src.data_ptr(), n, h, w, H, W, 0, out.data_ptr(), nv.stream())
+    return out
+
+
+def masks_uint8(x):
+    """(output * 255).astype(np.uint8) of test.py:317 (truncation toward zero)."""
+    return (x.detach().float().cpu().numpy() * 255).astype("uint8")

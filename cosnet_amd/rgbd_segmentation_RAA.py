@@ -143,14 +143,29 @@ class RGBDSegmentation_RAA(nn.Module):
         rgbs_a, rgbs_b, depths_a, depths_b = map(self._prep, (rgbs_a, rgbs_b, depths_a, depths_b))
         input_size = tuple(rgbs_a.shape[2:])
         ng = torch.no_grad if self.no_grad_for_counterpart else _Null
-        # RGB
         va, geo = self.encoder.features_nhwc(rgbs_a)
         with ng():
             vb, _ = self.encoder.features_nhwc(rgbs_b)
         with torch.no_grad():
             labels = self.encoder.annotate_nhwc(vb, geo, input_size)       # frame b (:146)
+        da, dgeo = self.depth_encoder.features_nhwc(depths_a)
+        with ng():
+            db, _ = self.depth_encoder.features_nhwc(depths_b)
+        if dgeo != geo:
+            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+        x1, x2 = self.head_nhwc(va, vb, da, db, geo, input_size)
+        if stages is not None:
+            stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
+        return x1, x2, labels
+
+    def head_nhwc(self, va, vb, da, db, geo, input_size):
+        """Co-attention (RGB and depth), gated fusion and decoder from encoder features
+        (rgbd_segmentation_RAA.py:150-266).  The reference interleaves the depth encoder calls
+        with the RGB head (:198-203); the encoders have no data dependence on the head, so the
+        order of launches does not change any result."""
         n, h, w = geo
         hw = h * w
+        # RGB co-attention
         za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw))
         cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False)
         cat_b = fn.GateCatFn.apply(zb, vb, self.gate.weight, None, True)  # mask_b no_grad (:178-182)
@@ -158,12 +173,7 @@ class RGBDSegmentation_RAA(nn.Module):
                             self.bn_A.weight, self.bn_A.bias, self.bn_A)
         z_b = fn.BNFn.apply(fn.ConvFn.apply(cat_b, self.reduce_channels_B.weight, None, geo, 3, 1, 1, 1),
                             self.bn_B.weight, self.bn_B.bias, self.bn_B)
-        # Depth
-        da, dgeo = self.depth_encoder.features_nhwc(depths_a)
-        with ng():
-            db, _ = self.depth_encoder.features_nhwc(depths_b)
-        if dgeo != geo:
-            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+        # depth co-attention
         dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw))
         dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False)
         dz_a = fn.BNFn.apply(fn.ConvFn.apply(dcat_a, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
@@ -181,9 +191,7 @@ class RGBDSegmentation_RAA(nn.Module):
                              self.segmentation_classifier_B.bias, True)
         x1 = fn.UpSigFn.apply(la, geo, input_size)
         x2 = fn.UpSigFn.apply(lb, geo, input_size)
-        if stages is not None:
-            stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
-        return x1, x2, labels
+        return x1, x2
 
 
 CoattentionModel = RGBDSegmentation_RAA  # name used by BASELINE.json's north_star
