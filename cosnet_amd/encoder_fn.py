@@ -1,0 +1,280 @@
+"""Both frames of one encoder in ONE batched pass: EncoderPairFn.
+
+The reference calls each encoder twice per step: once on frame a (with grad) and once on
+frame b under no_grad (rgbd_segmentation_RAA.py:143-148, :198-203).  Every op of the
+encoder is per-sample except BatchNorm's batch statistics, so frames a and b are stacked
+into one NHWC batch of 2N images: every GEMM runs with twice the rows (better MFMA tile
+occupancy, half the launches) while BN statistics and running-stat updates are computed per
+frame segment, a first then b, exactly as the two separate reference calls do.  The backward
+(hand-written, no per-block autograd nodes) runs on the frame-a rows only, which is all the
+reference differentiates.
+
+Reference blocks: stem deeplab/residual_net.py:157-160, Bottleneck :74-96, ASPP
+deeplab/deeplabv3_encoder.py:50-86.
+"""
+import torch
+
+from . import _native as nv
+from . import ops
+from .ops import WCACHE, as_param_grad, bn_apply, bn_bwd, bn_stats, conv_dgrad, conv_fwd, conv_wgrad
+
+F = torch.autograd.Function
+
+
+# ---- segment helpers -----------------------------------------------------------------------
+def seg_stats(x, bn, training, nseg):
+    """Per-segment (frame) BN statistics; running stats updated segment by segment."""
+    p = x.shape[0] // nseg
+    return [bn_stats(x[i * p:(i + 1) * p], bn, training) for i in range(nseg)]
+
+
+def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
+    nseg = len(stats)
+    p = x.shape[0] // nseg
+    if out is None:
+        out = torch.empty_like(x)
+    for i in range(nseg):
+        s = slice(i * p, (i + 1) * p)
+        bn_apply(x[s], stats[i], bn, act=act, prelu=prelu, res=None if res is None else res[s],
+                 xr=None if xr is None else xr[s], rstats=None if rstats is None else rstats[i],
+                 rbn=rbn, out=out[s])
+    return out
+
+
+# ---- stem --------------------------------------------------------------------------------------
+def stem_fwd(res, imgs, nseg, dt, rec):
+    n1, cimg, h, w = imgs[0].shape
+    n = n1 * len(imgs)
+    x = torch.empty((n * h * w, 8), dtype=dt, device=imgs[0].device)
+    for i, img in enumerate(imgs):
+        nv.call("cn_nchw_to_nhwc", nv.dtype_code(dt), img.data_ptr(), n1, cimg, h, w, 8,
+                x[i * n1 * h * w:].data_ptr(), nv.stream())
+    wf, _ = WCACHE.get(res.conv1.weight, dt, cin_pad=8, need_t=False)
+    c, oh, ow = conv_fwd(x, n, h, w, wf, 64, 7, 2, 3, 1)
+    st = seg_stats(c, res.bn1, res.training, nseg)
+    y = seg_apply(c, st, res.bn1, act=1)
+    ph, pw = ops.pool_out(oh), ops.pool_out(ow)
+    out = torch.empty((n * ph * pw, 64), dtype=dt, device=x.device)
+    am = torch.empty((n * ph * pw * 64,), dtype=torch.uint8, device=x.device)
+    nv.call("cn_maxpool_fwd", nv.dtype_code(dt), y.data_ptr(), n, oh, ow, 64, ph, pw, 3, 2, 1,
+            out.data_ptr(), am.data_ptr(), nv.stream())
+    if rec is not None:
+        rec.append(("stem", res, (x, c, y, am, st), (n1, cimg, h, w, oh, ow, ph, pw)))
+    return out, (n, ph, pw)
+
+
+def stem_bwd(item, dout, grads):
+    _, res, (x, c, y, am, st), (n1, cimg, h, w, oh, ow, ph, pw) = item
+    pa = n1 * oh * ow
+    dy = torch.empty((pa, 64), dtype=dout.dtype, device=dout.device)
+    nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n1, oh, ow, 64, ph,
+            pw, 3, 2, 1, dy.data_ptr(), nv.stream())
+    dc, dg, db, _ = bn_bwd(c[:pa], dy, y[:pa], st[0], res.bn1, act=1)
+    dw = conv_wgrad(x[:n1 * h * w], n1, h, w, 8, dc, oh, ow, 64, 7, 2, 3, 1)
+    grads[res.conv1.weight] = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
+    grads[res.bn1.weight] = dg
+    grads[res.bn1.bias] = db
+
+
+# ---- bottleneck ----------------------------------------------------------------------------------
+def bottleneck_fwd(blk, x, geo, nseg, rec):
+    n, h, w = geo
+    dt = x.dtype
+    tr = blk.training
+    s, d = blk.stride, blk.dilation
+    planes = blk.conv1.weight.shape[0]
+    w1f, w1t = WCACHE.get(blk.conv1.weight, dt)
+    w2f, w2t = WCACHE.get(blk.conv2.weight, dt)
+    w3f, w3t = WCACHE.get(blk.conv3.weight, dt)
+    c1, oh, ow = conv_fwd(x, n, h, w, w1f, planes, 1, s, 0, 1)
+    st1 = seg_stats(c1, blk.bn1, tr, nseg)
+    y1 = seg_apply(c1, st1, blk.bn1, act=1)
+    c2, _, _ = conv_fwd(y1, n, oh, ow, w2f, planes, 3, 1, d, d)
+    st2 = seg_stats(c2, blk.bn2, tr, nseg)
+    y2 = seg_apply(c2, st2, blk.bn2, act=1)
+    c3, _, _ = conv_fwd(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1)
+    st3 = seg_stats(c3, blk.bn3, tr, nseg)
+    cd = std = wdt = None
+    if blk.downsample is not None:
+        wdf, wdt = WCACHE.get(blk.downsample[0].weight, dt)
+        bnd = blk.downsample[1]
+        cd, _, _ = conv_fwd(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1)
+        std = seg_stats(cd, bnd, tr, nseg)
+        y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd)
+    else:
+        y = seg_apply(c3, st3, blk.bn3, act=1, res=x)
+    if rec is not None:
+        rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt),
+                    (n // nseg, h, w, oh, ow, s, d, planes, x.shape[1])))
+    return y, (n, oh, ow)
+
+
+def bottleneck_bwd(item, dy, grads, need_dx=True):
+    _, blk, sv, (n, h, w, oh, ow, s, d, planes, cin) = item
+    x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt = sv
+    pi, po = n * h * w, n * oh * ow                     # frame-a rows in / out
+    x, c1, y1, c2, y2, c3, y = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], y[:po]
+    has_down = cd is not None
+    dx = None
+    if has_down:
+        cd = cd[:po]
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1)
+        dcd, _, _, _ = bn_bwd(cd, dy, y, std[0], blk.downsample[1], act=1)
+    else:
+        dx = torch.empty_like(x)
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx)
+    dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
+    dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
+    dc2, dg2, db2, _ = bn_bwd(c2, dy2, y2, st2[0], blk.bn2, act=1)
+    dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
+    dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
+    dc1, dg1, db1, _ = bn_bwd(c1, dy1, y1, st1[0], blk.bn1, act=1)
+    dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
+    if need_dx:
+        dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
+    if has_down:
+        dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1)
+        grads[blk.downsample[0].weight] = as_param_grad(dwd, blk.downsample[0].weight)
+        if need_dx:
+            conv_dgrad(dcd, n, oh, ow, wdt, cin, 1, s, 0, 1, h, w, out=dx, accumulate=True)
+    grads[blk.conv1.weight] = as_param_grad(dw1, blk.conv1.weight)
+    grads[blk.conv2.weight] = as_param_grad(dw2, blk.conv2.weight)
+    grads[blk.conv3.weight] = as_param_grad(dw3, blk.conv3.weight)
+    grads[blk.bn1.weight], grads[blk.bn1.bias] = dg1, db1
+    grads[blk.bn2.weight], grads[blk.bn2.bias] = dg2, db2
+    grads[blk.bn3.weight], grads[blk.bn3.bias] = dg3, db3
+    return dx
+
+
+# ---- ASPP ------------------------------------------------------------------------------------------
+def aspp_fwd(mod, x, geo, nseg, rec):
+    n, h, w = geo
+    hw = h * w
+    P = n * hw
+    dt = x.dtype
+    tr = mod.training
+    dev = x.device
+    cat = torch.empty((P, 2560), dtype=dt, device=dev)
+    pool = torch.empty((n, 2048), dtype=dt, device=dev)
+    apws = torch.empty((n * 2048,), dtype=torch.float32, device=dev)
+    nv.call("cn_avgpool", ops.dtc(x), x.data_ptr(), ops.ld(x), n, hw, 2048, 1.0 / hw,
+            pool.data_ptr(), apws.data_ptr(), nv.stream())
+    wcf, wct = WCACHE.get(mod.conv.weight, dt)
+    cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=mod.conv.bias)
+    stp = seg_stats(cp, mod.bn_x, tr, nseg)
+    yp = seg_apply(cp, stp, mod.bn_x, act=1)
+    nv.call("cn_bcast_rows", ops.dtc(yp), yp.data_ptr(), n, hw, 512, 1.0, cat.data_ptr(), 2560, 0,
+            nv.stream())
+    convs = [(mod.conv2d_0, mod.bn_0, 1, 0)] + [
+        (getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)), 3, dd)
+        for i, dd in enumerate(mod.cn_dilations)]
+    cs, sts, wts = [], [], []
+    for bi, (cm, bnm, k, dd) in enumerate(convs):
+        wf, wt = WCACHE.get(cm.weight, dt)
+        ci, _, _ = conv_fwd(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bias=cm.bias)
+        st = seg_stats(ci, bnm, tr, nseg)
+        seg_apply(ci, st, bnm, act=1, out=cat[:, 512 * (bi + 1):512 * (bi + 2)])
+        cs.append(ci)
+        sts.append(st)
+        wts.append(wt)
+    wbf, wbt = WCACHE.get(mod.bottleneck.weight, dt)
+    cb, _, _ = conv_fwd(cat, n, h, w, wbf, 256, 3, 1, 1, 1, bias=mod.bottleneck.bias)
+    stb = seg_stats(cb, mod.bn, tr, nseg)
+    out = seg_apply(cb, stb, mod.bn, act=2, prelu=mod.prelu.weight)
+    if rec is not None:
+        rec.append(("aspp", mod, (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out),
+                    (n // nseg, h, w, [(k, dd) for (_, _, k, dd) in convs])))
+    return out
+
+
+def aspp_bwd(item, dout, grads):
+    _, mod, sv, (n, h, w, kd) = item
+    x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out = sv
+    hw = h * w
+    P = n * hw
+    x, cat, cb, out = x[:P], cat[:P], cb[:P], out[:P]
+    pool, cp, yp = pool[:n], cp[:n], yp[:n]
+    pw = mod.prelu.weight
+    dcb, dgb, dbb, dpr = bn_bwd(cb, dout, out, stb[0], mod.bn, act=2, prelu=pw)
+    grads[mod.bottleneck.weight] = as_param_grad(
+        conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1), mod.bottleneck.weight)
+    grads[mod.bottleneck.bias] = ops.colsum(dcb)
+    grads[mod.bn.weight], grads[mod.bn.bias], grads[pw] = dgb, dbb, dpr
+    dcat = conv_dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, 1, h, w)
+    dx = None
+    bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
+    cms = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
+    for bi, ((k, dd), ci, st, wt) in enumerate(zip(kd, cs, sts, wts)):
+        sl = slice(512 * (bi + 1), 512 * (bi + 2))
+        dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], cat[:, sl], st[0], bns[bi], act=1)
+        grads[cms[bi].weight] = as_param_grad(
+            conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1)), cms[bi].weight)
+        grads[cms[bi].bias] = ops.colsum(dci)
+        grads[bns[bi].weight], grads[bns[bi].bias] = dgi, dbi
+        dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
+                        accumulate=dx is not None)
+    dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
+    apws = torch.empty((n * 512,), dtype=torch.float32, device=dout.device)
+    nv.call("cn_avgpool", ops.dtc(dcat), dcat.data_ptr(), ops.ld(dcat), n, hw, 512, 1.0,
+            dyp.data_ptr(), apws.data_ptr(), nv.stream())
+    dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp[0], mod.bn_x, act=1)
+    grads[mod.conv.weight] = as_param_grad(conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1),
+                                           mod.conv.weight)
+    grads[mod.conv.bias] = ops.colsum(dcp)
+    grads[mod.bn_x.weight], grads[mod.bn_x.bias] = dgx, dbx
+    dpool = conv_dgrad(dcp, n, 1, 1, wct, 2048, 1, 1, 0, 1, 1, 1)
+    nv.call("cn_bcast_rows", ops.dtc(dpool), dpool.data_ptr(), n, hw, 2048, 1.0 / hw,
+            dx.data_ptr(), ops.ld(dx), 1, nv.stream())
+    return dx
+
+
+# ---- the Function -----------------------------------------------------------------------------
+class EncoderPairFn(F):
+    """EncoderPairFn.apply(img_a, img_b, enc, *enc_params) -> (feats_a, feats_b),
+    [N*h*w, 256] NHWC each; feats_b carries no gradient (the reference's no_grad call)."""
+
+    @staticmethod
+    def forward(ctx, img_a, img_b, enc, *params):
+        dt = getattr(enc, "_cn_dtype", torch.bfloat16)
+        rec = [] if any(ctx.needs_input_grad[3:]) else None
+        nseg = 2
+        x, geo = stem_fwd(enc.backbone, (img_a, img_b), nseg, dt, rec)
+        for layer in (enc.backbone.layer1, enc.backbone.layer2, enc.backbone.layer3, enc.backbone.layer4):
+            for blk in layer:
+                x, geo = bottleneck_fwd(blk, x, geo, nseg, rec)
+        out = aspp_fwd(enc.aspp, x, geo, nseg, rec)
+        half = out.shape[0] // 2
+        ctx.rec = rec
+        ctx.params = params
+        ctx.training = enc.training
+        ctx.set_materialize_grads(False)
+        fa, fb = out[:half], out[half:]
+        ctx.mark_non_differentiable(fb)
+        return fa, fb
+
+    @staticmethod
+    def backward(ctx, dfa, dfb):
+        rec = ctx.rec
+        if rec is None or dfa is None:
+            return (None,) * (3 + len(ctx.params))
+        if not ctx.training:
+            raise RuntimeError("backward through BatchNorm is implemented for train mode only")
+        grads = {}
+        dx = aspp_bwd(rec[-1], dfa if dfa.stride(1) == 1 else dfa.contiguous(), grads)
+        for item in reversed(rec[1:-1]):
+            dx = bottleneck_bwd(item, dx, grads)
+        stem_bwd(rec[0], dx, grads)
+        ctx.rec = None
+        return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
+
+
+def encode_pair(enc, img_a, img_b):
+    """(features of frame a, features of frame b, (n, h, w)) for one encoder."""
+    params = list(enc.parameters())
+    fa, fb = EncoderPairFn.apply(img_a, img_b, enc, *params)
+    n = img_a.shape[0]
+    h, w = img_a.shape[2], img_a.shape[3]
+    oh, ow = ops.out_hw(h, w, 7, 2, 3, 1)
+    ph, pw = ops.pool_out(oh), ops.pool_out(ow)
+    fh, fw = ops.out_hw(ph, pw, 1, 2, 0, 1)  # layer2 stride 2; layers 3-4 keep the size
+    return fa, fb, (n, fh, fw)
