@@ -50,6 +50,7 @@ _SIGS = {
     "cn_count_ge": (_I, [_P, _L, _F, _P, _P]),
     "cn_loss_workspace_floats": (_S, [_L]),
     "cn_bce_l1": (_I, [_P, _P, _L, _F, _F, _P, _P, _P, _P]),
+    "cn_bce_l1_devcount": (_I, [_P, _P, _L, _P, ctypes.c_double, _F, _P, _P, _P, _P]),
     "cn_sgd": (_I, [_P, _I, _P, _F, _F, _P]),
     "cn_rowdot": (_I, [_I, _P, _L, _P, _L, _I, _I, _P, _P]),
     "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P]),

@@ -437,7 +437,12 @@ __global__ void count_ge_k(const float* __restrict__ gt, long long n, float thr,
 // partial[block] = sum of per-element loss; dpred = d loss / d pred (already / n, * gscale)
 __global__ void bce_l1_k(const float* __restrict__ p, const float* __restrict__ y, long long n,
                          float weight, float l1w, float* __restrict__ partial,
-                         float* __restrict__ dpred) {
+                         float* __restrict__ dpred, const long long* __restrict__ pos_cnt,
+                         double total) {
+  if (pos_cnt) {  // weight = N*H*W / #(gt >= 0.5) from a device-side count (no host sync)
+    long long c = *pos_cnt;
+    weight = c > 0 ? (float)(total / (double)c) : 1.f;
+  }
   float acc = 0.f;
   const float invn = 1.f / (float)n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
@@ -724,7 +729,20 @@ extern "C" size_t cn_loss_workspace_floats(long long n) { return (size_t)nblocks
 extern "C" int cn_bce_l1(const float* pred, const float* gt, long long n, float weight, float l1w,
                          float* ws, float* loss, float* dpred, hipStream_t st) {
   int nb = nblocks(n, 1024);
-  hipLaunchKernelGGL(bce_l1_k, dim3(nb), dim3(256), 0, st, pred, gt, n, weight, l1w, ws, dpred);
+  hipLaunchKernelGGL(bce_l1_k, dim3(nb), dim3(256), 0, st, pred, gt, n, weight, l1w, ws, dpred,
+                     (const long long*)nullptr, 0.0);
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials_k, dim3(1), dim3(64), 0, st, ws, nb, 1.0f / (float)n, loss);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bce_l1_devcount(const float* pred, const float* gt, long long n,
+                                  const long long* pos_count, double total, float l1w, float* ws,
+                                  float* loss, float* dpred, hipStream_t st) {
+  int nb = nblocks(n, 1024);
+  hipLaunchKernelGGL(bce_l1_k, dim3(nb), dim3(256), 0, st, pred, gt, n, 1.f, l1w, ws, dpred,
+                     pos_count, total);
   CN_CHECK_LAUNCH();
   hipLaunchKernelGGL(sum_partials_k, dim3(1), dim3(64), 0, st, ws, nb, 1.0f / (float)n, loss);
   CN_CHECK_LAUNCH();

@@ -468,6 +468,29 @@ class UpSigFn(F):
         return dl, None, None
 
 
+class BceL1DevFn(F):
+    """BceL1Fn with the BCE weight N*H*W / #pos taken from a device count tensor (int64 [1]):
+    no host synchronisation, so the whole train step can be captured in a HIP graph."""
+
+    @staticmethod
+    def forward(ctx, pred, gt, pos_count, total, l1w):
+        pred = pred.contiguous()
+        gt = gt.contiguous()
+        n = pred.numel()
+        ws = torch.empty((int(nv.query("cn_loss_workspace_floats", n)),), dtype=torch.float32,
+                         device=pred.device)
+        loss = torch.empty((), dtype=torch.float32, device=pred.device)
+        dpred = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        nv.call("cn_bce_l1_devcount", pred.data_ptr(), gt.data_ptr(), n, pos_count.data_ptr(),
+                float(total), float(l1w), ws.data_ptr(), loss.data_ptr(), nv.ptr(dpred), nv.stream())
+        ctx.dpred = dpred
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        return ctx.dpred * gout, None, None, None, None
+
+
 class BceL1Fn(F):
     """weight * BCE(pred, gt) + l1w * L1(pred, gt), means over all elements (train.py:176-216)."""
 

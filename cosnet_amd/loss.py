@@ -49,3 +49,15 @@ def bce_l1(pred, label, ratio="auto", l1_weight=0.8):
         ratio = positive_ratio(label)
     w = 1.0 if ratio is None else ratio
     return fn.BceL1Fn.apply(pred, label, w, l1_weight)
+
+
+def bce_l1_device(pred, label, l1_weight=0.8, group=None):
+    """bce_l1 with the positive count kept on the device (all-reduced asynchronously under
+    DDP): no host sync, HIP-graph capturable.  Same value as bce_l1."""
+    cnt = fn.count_positive(label)
+    n, _, h, w = label.shape
+    total = n * h * w
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(cnt, group=group)
+        total *= dist.get_world_size(group)
+    return fn.BceL1DevFn.apply(pred, label, cnt, total, l1_weight)

@@ -124,6 +124,10 @@ int cn_count_ge(const float* gt, long long n, float thr, unsigned long long* cnt
 size_t cn_loss_workspace_floats(long long n);
 int cn_bce_l1(const float* pred, const float* gt, long long n, float weight, float l1w, float* ws,
               float* loss, float* dpred, hipStream_t stream);
+/* same, with the BCE weight N*H*W/#pos read from a device-side count (capturable, no sync) */
+int cn_bce_l1_devcount(const float* pred, const float* gt, long long n, const long long* pos_count,
+                       double total, float l1w, float* ws, float* loss, float* dpred,
+                       hipStream_t stream);
 /* optim.SGD(momentum, weight_decay) step over a device table of tensors: train.py:538-540,602 */
 int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float momentum,
            hipStream_t stream);

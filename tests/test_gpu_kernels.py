@@ -321,11 +321,20 @@ def test_loss_bce_l1(cuda):
     torch.cuda.synchronize()
     assert abs(out.item() - ref.item()) <= 1e-5 * abs(ref.item())
     close(pg.grad, pr.grad, torch.float32)
+    # device-count variant (no host sync) gives the same loss and gradient
+    pg2 = pred.float().to(cuda).requires_grad_(True)
+    out2 = L.bce_l1_device(pg2, gt.float().to(cuda))
+    out2.backward()
+    torch.cuda.synchronize()
+    assert abs(out2.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    close(pg2.grad, pr.grad, torch.float32)
     # empty GT -> unweighted BCE (train.py:185-187)
     z = torch.zeros_like(gt)
     ref0 = F.binary_cross_entropy(pred, z) + 0.8 * F.l1_loss(pred, z)
     out0 = L.bce_l1(pred.float().to(cuda), z.float().to(cuda))
     assert abs(out0.item() - ref0.item()) <= 1e-5 * abs(ref0.item())
+    out0d = L.bce_l1_device(pred.float().to(cuda), z.float().to(cuda))
+    assert abs(out0d.item() - ref0.item()) <= 1e-5 * abs(ref0.item())
 
 
 def test_sgd_step(cuda):
