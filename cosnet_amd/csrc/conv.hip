@@ -87,47 +87,80 @@ extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, i
   return cn_gemm_dispatch(a, dtype, 0, L_KC_DENSE, L_KC_DENSE, 1, st);
 }
 
-static int pick_splits(int tiles, int K, int BK) {
-  // aim for ~2 waves of 256 CUs, keep each split >= 4 K-tiles
-  int want = (512 + tiles - 1) / tiles;
-  int maxs = K / (4 * BK);
+static int pick_splits(long long tiles, int K, int BK) {
+  // ~512 blocks (2 per CU) but every split keeps >= 8 K-tiles of work
+  long long want = (512 + tiles - 1) / tiles;
+  long long maxs = K / (8 * BK);
   if (maxs < 1) maxs = 1;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
-  return want;
+  return (int)want;
+}
+
+static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
+                       int* chunk) {
+  int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
+  int BK = 8 * vec_of(dtype);
+  long long t128 = (long long)((M + 127) / 128) * ((NN + 127) / 128);
+  long long tiles = (NN <= 64 || t128 < 384) ? (long long)((M + 127) / 128) * ((NN + 63) / 64) : t128;
+  int ns = pick_splits(tiles, K, BK);
+  int ch = (K + ns - 1) / ns;
+  ch = (ch + BK - 1) / BK * BK;
+  *nsplit = (K + ch - 1) / ch;
+  *chunk = ch;
+}
+
+extern "C" size_t cn_conv_wgrad_workspace_floats(int dtype, int N, int OH, int OW, int Cout, int KH,
+                                                 int KW, int Cin) {
+  int ns, ch;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch);
+  return ns > 1 ? (size_t)ns * Cout * KH * KW * Cin : 0;
 }
 
 extern "C" int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                              const void* dy, long long lddy, int OH, int OW, int Cout, int KH,
-                             int KW, int stride, int pad, int dil, float* dw, hipStream_t st) {
+                             int KW, int stride, int pad, int dil, float* dw, float* ws,
+                             hipStream_t st) {
   if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
   GemmArgs a = gemm_defaults();
   a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
   a.ka_lim = a.kb_lim = a.K;
   a.A = dy; a.lda = lddy;
   a.B = x; a.ldb = ldx;
-  a.C = dw; a.ldc = a.N;
-  a.c_mode = 1;  // fp32 atomics (split-K); dw must be zeroed by the caller
+  a.ldc = a.N;
   int lb = L_MC_DENSE;
   if (!(KH == 1 && KW == 1 && stride == 1 && pad == 0)) {
     lb = L_MC_CONV;
     a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
   }
-  int BK = 8 * vec_of(dtype);
-  int tiles = ((a.M + 127) / 128) * ((a.N + (a.N <= 64 ? 63 : 127)) / (a.N <= 64 ? 64 : 128));
-  int ns = pick_splits(tiles, a.K, BK);
-  int chunk = (a.K + ns - 1) / ns;
-  chunk = (chunk + BK - 1) / BK * BK;
-  a.nsplit = (a.K + chunk - 1) / chunk;
-  a.k_chunk = chunk;
-  return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, 1, st);
+  int ns, ch;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch);
+  a.nsplit = ns;
+  a.k_chunk = ch;
+  if (ns == 1) {  // whole K in one block: write dw directly
+    a.C = dw;
+    return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, 1, st);
+  }
+  if (!ws) return CN_ERR_SHAPE;
+  // split-K partials into fp32 slabs (plain stores, no atomics), then a fixed-order sum
+  a.C = ws;
+  a.c_mode = 3;
+  a.slab = (long long)a.M * a.N;
+  int rc = cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, 1, st);
+  if (rc) return rc;
+  return cn_splitk_reduce_impl(ws, ns, a.slab, a.slab, dw, 0, st);
+}
+
+extern "C" int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
+                                int accumulate, hipStream_t st) {
+  return cn_splitk_reduce_impl(ws, nsplit, slab, n, out, accumulate, st);
 }
 
 extern "C" int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int K, int ka_lim,
                        int kb_lim, const void* A, long long lda, long long a_bs, const void* B,
                        long long ldb, long long b_bs, void* C, long long ldc, long long c_bs,
                        int c_f32, int c_mode, float alpha, const float* bias, int batch,
-                       int nsplit, hipStream_t st) {
+                       int nsplit, long long slab, hipStream_t st) {
   GemmArgs a = gemm_defaults();
   a.M = M; a.N = N; a.K = K;
   a.ka_lim = ka_lim; a.kb_lim = kb_lim;
@@ -137,7 +170,8 @@ extern "C" int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int 
   a.bias = bias;
   a.alpha = alpha;
   a.c_mode = c_mode;
-  if (c_mode == 1 && !c_f32) return CN_ERR_UNSUPPORTED;
+  a.slab = slab;
+  if ((c_mode == 1 || c_mode == 3) && !c_f32) return CN_ERR_UNSUPPORTED;
   if (nsplit > 1) {
     int BK = 8 * vec_of(dtype);
     int chunk = (K + nsplit - 1) / nsplit;

@@ -31,8 +31,12 @@ struct GemmArgs {
   int row_map;                 // 1: stride-2 dgrad scatter of output rows
   FastDiv rm_div_OW, rm_div_OHW;
   int rm_H, rm_W;
-  int c_mode;                  // 0 store, 1 fp32 atomic add, 2 read-add-store
+  int c_mode;                  // 0 store, 1 fp32 atomic add, 2 read-add-store,
+                               // 3 split-K slab store (C + split * slab)
+  long long slab;              // elements between split-K slabs (c_mode 3)
   float alpha;
 };
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);
+int cn_splitk_reduce_impl(const float* ws, int nsplit, long long slab, long long n, float* out,
+                          int accumulate, hipStream_t st);

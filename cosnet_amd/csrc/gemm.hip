@@ -380,7 +380,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
   constexpr int HR = BM / 2;
   static_assert(HR * LDC * 4 <= 2 * STAGE, "epilogue staging must fit in the LDS image");
   float* cs = (float*)smem;
-  CT* Cb = (CT*)p.C + (long long)batch * p.c_bs;
+  CT* Cb = (CT*)p.C + (long long)batch * p.c_bs + (p.c_mode == 3 ? (long long)split * p.slab : 0);
+  const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
   constexpr int GPR = BN / 8;            // 8-column groups per row
   constexpr int RPP = NT / GPR;          // rows per pass
 #pragma unroll 1
@@ -419,13 +420,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += (col + e < p.N) ? p.bias[col + e] : 0.f;
       }
-      if (p.c_mode == 1) {
+      if (cmode == 1) {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (col + e < p.N) store_c<CT>(dst + e, v[e], 1);
       } else if (full) {
         if constexpr (sizeof(CT) == 2) {
-          if (p.c_mode == 2) {
+          if (cmode == 2) {
             float q[8];
             Chunk<bf16>::unpack(*(const u32x4*)dst, q);
 #pragma unroll
@@ -433,7 +434,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
           }
           *(u32x4*)dst = Chunk<bf16>::pack(v);
         } else {
-          if (p.c_mode == 2) {
+          if (cmode == 2) {
             f32x4 q0 = *(const f32x4*)dst, q1 = *(const f32x4*)(dst + 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) { v[e] += q0[e]; v[4 + e] += q1[e]; }
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (col + e < p.N) store_c<CT>(dst + e, v[e], p.c_mode);
+          if (col + e < p.N) store_c<CT>(dst + e, v[e], cmode);
       }
     }
     __syncthreads();
@@ -492,4 +493,30 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     return launch_kinds<float, float>(a, la, lb, batch, st);
   }
   return -11;
+}
+
+// Split-K reduction: out[i] (+)= sum_s ws[s * slab + i]  (fp32, float4-vectorised, fixed order
+// so the result is bitwise reproducible).
+__global__ void splitk_reduce_k(const float* __restrict__ ws, int nsplit, long long slab,
+                                long long n4, float* __restrict__ out, int accumulate) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a = accumulate ? ((const f32x4*)out)[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < nsplit; ++s) {
+      f32x4 b = *(const f32x4*)(ws + s * slab + 4 * i);
+      a += b;
+    }
+    ((f32x4*)out)[i] = a;
+  }
+}
+
+int cn_splitk_reduce_impl(const float* ws, int nsplit, long long slab, long long n, float* out,
+                          int accumulate, hipStream_t st) {
+  if (n % 4 || slab % 4) return -2;
+  long long n4 = n / 4;
+  long long b = (n4 + 255) / 256;
+  if (b > 2048) b = 2048;
+  hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)b), dim3(256), 0, st, ws, nsplit, slab, n4, out, accumulate);
+  CN_CHECK_LAUNCH();
+  return 0;
 }

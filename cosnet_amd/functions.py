@@ -321,10 +321,10 @@ class CoattFn(F):
                      c_mode=mode)
         dw = None
         if ctx.needs_input_grad[2]:
-            dw = torch.zeros((c, c), dtype=torch.float32, device=dev)
+            dw = torch.empty((c, c), dtype=torch.float32, device=dev)
             ns = max(1, min(64, P // 512))
             ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
-                     ldb=ops.ld(va), out=dw, ldc=c, c_mode=1, nsplit=ns)
+                     ldb=ops.ld(va), out=dw, ldc=c, c_mode=0, nsplit=ns)
         return dva, None, dw, None
 
 

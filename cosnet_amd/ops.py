@@ -134,12 +134,14 @@ def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accu
 
 
 def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
-    """fp32 [cout, k*k*cin] weight gradient (channels_last order)."""
+    """fp32 [cout, k*k*cin] weight gradient (channels_last order), fully overwritten."""
     if dw is None:
-        dw = torch.zeros((cout, k * k * cin), dtype=torch.float32, device=x.device)
+        dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
+    nws = int(nv.query("cn_conv_wgrad_workspace_floats", dtc(x), n, oh, ow, cout, k, k, cin))
+    ws = torch.empty((nws,), dtype=torch.float32, device=x.device) if nws else None
     ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
     nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
-            ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.stream())
+            ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.ptr(ws), nv.stream())
     _prof_end(ev)
     return dw
 
@@ -173,12 +175,31 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
         c_bs = m * n
     c_f32 = int(out.dtype == torch.float32)
     ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k))
-    nv.call("cn_gemm", nv.dtype_code(dt), layout_a, layout_b, m, n, k,
-            k if ka_lim is None else ka_lim, k if kb_lim is None else kb_lim,
-            a.data_ptr(), lda, a_bs, b.data_ptr(), ldb, b_bs, out.data_ptr(), ldc, c_bs, c_f32,
-            c_mode, float(alpha), nv.ptr(bias), batch, nsplit, nv.stream())
+    if nsplit > 1 and c_mode in (0, 1) and batch == 1 and c_f32 and ldc == n:
+        # split-K into fp32 slabs + fixed-order reduction (no atomic contention)
+        slab = m * n
+        ws = torch.empty((nsplit * slab,), dtype=torch.float32, device=a.device)
+        nv.call("cn_gemm", nv.dtype_code(dt), layout_a, layout_b, m, n, k,
+                k if ka_lim is None else ka_lim, k if kb_lim is None else kb_lim,
+                a.data_ptr(), lda, a_bs, b.data_ptr(), ldb, b_bs, ws.data_ptr(), ldc, 0, 1,
+                3, float(alpha), None, 1, nsplit, slab, nv.stream())
+        nv.call("cn_splitk_reduce", ws.data_ptr(), _nsplit_eff(k, nsplit, dt), slab, slab,
+                out.data_ptr(), int(c_mode == 1), nv.stream())
+    else:
+        nv.call("cn_gemm", nv.dtype_code(dt), layout_a, layout_b, m, n, k,
+                k if ka_lim is None else ka_lim, k if kb_lim is None else kb_lim,
+                a.data_ptr(), lda, a_bs, b.data_ptr(), ldb, b_bs, out.data_ptr(), ldc, c_bs, c_f32,
+                c_mode, float(alpha), nv.ptr(bias), batch, nsplit, 0, nv.stream())
     _prof_end(ev)
     return out
+
+
+def _nsplit_eff(k, nsplit, dt):
+    """Number of splits cn_gemm really launches (chunks rounded up to whole K tiles)."""
+    bk = 64 if dt == torch.bfloat16 else 32
+    chunk = -(-k // nsplit)
+    chunk = -(-chunk // bk) * bk
+    return -(-k // chunk)
 
 
 # ---- batch norm -------------------------------------------------------------------------------

@@ -51,9 +51,10 @@ class SGD:
         self.momentum = float(momentum)
         self.weight_decay = float(weight_decay)
         self.state = {}
-        self._table = None
+        self._tables = []
         self._table_key = None
         self._lr_dev = None
+        self._lr_static = False
 
     def zero_grad(self, set_to_none=True):
         for g in self.groups:
@@ -94,8 +95,8 @@ class SGD:
         if not recs:
             return
         dev = self.groups[0][0].device if self.groups[0] else self.groups[1][0].device
-        # one launch per "generation" of first-step flags so duplicates apply sequentially
-        # (a parameter listed k times is updated k times, like torch's for-loop SGD)
+        # one launch per "generation" so a parameter listed k times is updated k times in
+        # order (torch's for-loop SGD over duplicated param-group entries)
         batches, cur, seen = [], [], set()
         for r in recs:
             if r[0] in seen:
@@ -104,15 +105,40 @@ class SGD:
             cur.append(r)
             seen.add(r[0])
         batches.append(cur)
-        lr = torch.tensor(self.lrs, dtype=torch.float32).to(dev, non_blocking=True)
-        self._lr_dev = lr
-        for b in batches:
-            blob = b"".join(_REC.pack(*r) for r in b)
-            tab = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev, non_blocking=True)
-            nv.call("cn_sgd", tab.data_ptr(), len(b), lr.data_ptr(), self.weight_decay,
+        self._upload_lrs(dev)
+        key = tuple(tuple(b) for b in batches)
+        if key != self._table_key:
+            # device tables of SgdTensor records, staged through pinned memory so the copy is
+            # asynchronous and capturable; rebuilt only when a pointer / flag changes
+            self._tables = []
+            for b in batches:
+                blob = b"".join(_REC.pack(*r) for r in b)
+                host = torch.frombuffer(bytearray(blob), dtype=torch.uint8).pin_memory()
+                devt = torch.empty_like(host, device=dev)
+                devt.copy_(host, non_blocking=True)
+                self._tables.append((host, devt, len(b)))
+            self._table_key = key
+        for host, devt, nrec in self._tables:
+            nv.call("cn_sgd", devt.data_ptr(), nrec, self._lr_dev.data_ptr(), self.weight_decay,
                     self.momentum, nv.stream())
-            self._table = tab  # keep alive until the stream consumes it
         WeightCache.epoch += 1
+
+    def _upload_lrs(self, dev):
+        if self._lr_dev is None:
+            self._lr_dev = torch.empty((len(self.lrs),), dtype=torch.float32, device=dev)
+        if self._lr_static:
+            return  # refreshed outside a captured graph by refresh_lrs()
+        self.refresh_lrs()
+
+    def refresh_lrs(self):
+        """Copy the current learning rates into the device tensor the SGD kernel reads.  A fresh
+        pinned buffer per call: torch's caching host allocator keeps it until the copy ran."""
+        host = torch.tensor(self.lrs, dtype=torch.float32).pin_memory()
+        self._lr_dev.copy_(host, non_blocking=True)
+
+    def freeze_for_capture(self):
+        """After this, step() no longer re-uploads learning rates (use refresh_lrs())."""
+        self._lr_static = True
 
 
 def _fmt(p):

@@ -43,19 +43,28 @@ int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, int OH, int 
                   const void* wt, int Cin, int KH, int KW, int stride, int pad, int dil,
                   void* dx, long long lddx, int H, int W, int accumulate, hipStream_t stream);
 
-/* dw[Cout][KH][KW][Cin] += conv2d weight-gradient (fp32, split-K atomics; zero dw first). */
+/* dw[Cout][KH][KW][Cin] = conv2d weight-gradient (fp32).  K (= output pixels) is split over
+ * workgroups; partial products go to `ws` slabs (cn_conv_wgrad_workspace_floats; may be 0)
+ * and are summed in a fixed order (bitwise reproducible, no atomics). */
+size_t cn_conv_wgrad_workspace_floats(int dtype, int N, int OH, int OW, int Cout, int KH, int KW,
+                                      int Cin);
 int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                   const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
-                  int stride, int pad, int dil, float* dw, hipStream_t stream);
+                  int stride, int pad, int dil, float* dw, float* ws, hipStream_t stream);
+/* out[i] (+)= sum_s ws[s*slab + i], s < nsplit  (split-K reduction, fp32) */
+int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
+                     int accumulate, hipStream_t stream);
 
 /* Generic batched C = alpha * A . B^T (+bias) with per-operand layouts
  * (0 = k-contiguous rows, 2 = m/n-contiguous, k-major).  Replaces the linear + bmm calls of
  * the co-attention: rgbd_segmentation_RAA.py:159-160,169-170 (RGB) and :212-213,220-221
- * (depth), and their autograd.  c_mode: 0 store, 1 fp32 atomic add, 2 accumulate. */
+ * (depth), and their autograd.  c_mode: 0 store, 1 fp32 atomic add, 2 accumulate,
+ * 3 split-K slabs at C + split*slab (reduce with cn_splitk_reduce). */
 int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int K, int ka_lim, int kb_lim,
             const void* A, long long lda, long long a_bs, const void* B, long long ldb,
             long long b_bs, void* C, long long ldc, long long c_bs, int c_f32, int c_mode,
-            float alpha, const float* bias, int batch, int nsplit, hipStream_t stream);
+            float alpha, const float* bias, int batch, int nsplit, long long slab,
+            hipStream_t stream);
 
 /* ---- BatchNorm2d (train: batch stats + running update; eval: running stats) ---------- */
 size_t cn_bn_workspace_floats(int dtype, int P, int C);
