@@ -291,7 +291,22 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // XCD-aware tile order (guide §5.5 T1, bijective form): blocks are dealt round-robin over
+  // the 8 XCDs, so remap the linear id to give every XCD a contiguous run of M-tiles that
+  // share the same B (weight) panel in its private L2.
+  int tm, tn;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    const int orig = blockIdx.x + blockIdx.y * gridDim.x;
+    int lin = orig;
+    if (nwg >= 16) {
+      const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+      lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    }
+    tm = lin % gridDim.x;
+    tn = lin / gridDim.x;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
   const int bz = blockIdx.z;
   const int batch = bz / p.nsplit, split = bz - batch * p.nsplit;
   const int kbeg = split * p.k_chunk;
