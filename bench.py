@@ -46,7 +46,13 @@ def cpu_baseline(size):
     from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
     import cosnet_amd as C
     from oracle.model_ref import RefModel, loss_bce_l1
-    threads = os.cpu_count() or 1
+    # the cores this process may actually use (the GPU box reports the whole host in
+    # os.cpu_count() but grants a share: OMP_NUM_THREADS / the affinity mask)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
     torch.set_num_threads(threads)
     tmpl = C.build_model().state_dict()
     ref = RefModel(recipe_state_dict(tmpl), dtype=torch.float32)

@@ -110,14 +110,25 @@ __global__ __launch_bounds__(1024) void bn_stats_finalize(const float* __restric
   const int lane = threadIdx.x >> 6;
   float cn = 0.f, cm = 0.f, c2 = 0.f;
   if (c < C) {
-    for (int s = lane; s < S; s += 16) {
-      const float* w = ws + ((long long)s * C + c) * 3;
-      float nb = w[0], mb = w[1], qb = w[2];
-      if (nb == 0.f) continue;
-      float nn = cn + nb, d = mb - cm, r = nb / nn;
-      cm = fmaf(d, r, cm);
-      c2 += qb + d * d * cn * r;
-      cn = nn;
+    // 4 partials loaded per round (independent loads in flight), then merged in order
+    for (int s0 = lane; s0 < S; s0 += 64) {
+      float pn[4], pm[4], pq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = s0 + 16 * u;
+        const float* w = ws + ((long long)(s < S ? s : 0) * C + c) * 3;
+        pn[u] = s < S ? w[0] : 0.f;
+        pm[u] = w[1];
+        pq[u] = w[2];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pn[u] == 0.f) continue;
+        float nn = cn + pn[u], d = pm[u] - cm, r = pn[u] / nn;
+        cm = fmaf(d, r, cm);
+        c2 += pq[u] + d * d * cn * r;
+        cn = nn;
+      }
     }
   }
   __shared__ float sn[16][64], sm[16][64], s2[16][64];
@@ -291,9 +302,19 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict_
   const int lane = threadIdx.x >> 6;
   float a = 0.f, b = 0.f, d = 0.f;
   if (c < C) {
-    for (int s = lane; s < S; s += 16) {
-      const float* w = ws + ((long long)s * C + c) * 3;
-      a += w[0]; b += w[1]; d += w[2];
+    for (int s0 = lane; s0 < S; s0 += 64) {
+      float pa[4], pb[4], pd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int s = s0 + 16 * u;
+        const float* w = ws + ((long long)(s < S ? s : 0) * C + c) * 3;
+        const bool ok = s < S;
+        pa[u] = ok ? w[0] : 0.f;
+        pb[u] = ok ? w[1] : 0.f;
+        pd[u] = ok ? w[2] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a += pa[u]; b += pb[u]; d += pd[u]; }
     }
   }
   __shared__ float ra[16][64], rb[16][64], rd[16][64];
