@@ -12,7 +12,8 @@
 
 namespace {
 
-constexpr int UNR = 4;  // rows in flight per thread in the streaming loops
+constexpr int UNR = 4;   // rows in flight per thread in the streaming (apply) loops
+constexpr int SUNR = 8;  // rows in flight per thread in the statistics pass
 
 struct Layout {
   int CPR, CB, RPB;
@@ -32,7 +33,105 @@ template <class T> __device__ __forceinline__ void st_chunk(T* p, const float* f
   *(u32x4*)p = Chunk<T>::pack(f);
 }
 
-// ---- forward statistics: shifted sums per thread -> (n, mean, M2) -> Chan merge ----------
+// Column sums of the block's RPB rows of per-thread accumulators, written as
+// out[q][blockIdx.y][c] (q < NQ planes of S x C floats).  Parallel over all 256 threads: with
+// NCOL = CB*V columns, 256/NCOL partial sums per column, then one more pass.
+template <int V, int NQ>
+__device__ __forceinline__ void block_col_sums(const Layout& L, int tx, int ty, const float* a,
+                                               const float* b, const float* c3, float* out,
+                                               int S, int C) {
+  __shared__ float red[NQ][256 * 8];
+  const int NCOL = L.CB * V;
+  if (ty < L.RPB) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      red[0][ty * NCOL + tx * V + v] = a[v];
+      if (NQ > 1) red[1][ty * NCOL + tx * V + v] = b[v];
+      if (NQ > 2) red[NQ > 2 ? 2 : 0][ty * NCOL + tx * V + v] = c3[v];
+    }
+  }
+  __syncthreads();
+  const int c0 = blockIdx.x * NCOL;
+  const long long plane = (long long)S * C;
+  float* o = out + (long long)blockIdx.y * C + c0;
+  if (NCOL >= 256) {
+    for (int j = threadIdx.x; j < NCOL; j += 256) {
+      float acc[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+      for (int k = 0; k < L.RPB; ++k)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += red[q][k * NCOL + j];
+      if (c0 + j < C)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) o[q * plane + j] = acc[q];
+    }
+  } else {
+    const int np = 256 / NCOL, part = threadIdx.x / NCOL, j = threadIdx.x % NCOL;
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    if (part < np)
+      for (int k = part; k < L.RPB; k += np)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += red[q][k * NCOL + j];
+    __syncthreads();
+    if (part < np)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) red[q][part * NCOL + j] = acc[q];
+    __syncthreads();
+    if (threadIdx.x < NCOL && c0 + j < C) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float t = 0.f;
+        for (int k = 0; k < np; ++k) t += red[q][k * NCOL + j];
+        o[q * plane + j] = t;
+      }
+    }
+  }
+}
+
+// Sum over the S splits of npl consecutive planes of S x C partials, for the FCH channels of
+// this block: thread = (channel tid % FCH, lane tid / FCH), 32 lanes stride the splits, then
+// shuffles over the 8 lanes of a wave and an LDS pass over the 4 waves.  tot[plane][FCH].
+constexpr int FCH = 8, MAXPL = 8;
+template <int NPL>
+__device__ __forceinline__ void plane_sums(const float* __restrict__ ws, int S, int C, int c0,
+                                           float (*tot)[FCH]) {
+  constexpr int npl = NPL;  // compile-time so every plane's load is issued unconditionally
+  const int ch = threadIdx.x % FCH, lane = threadIdx.x / FCH, c = c0 + ch;
+  const long long plane = (long long)S * C;
+  float acc[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) acc[q] = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int s = lane; s < S; s += 256 / FCH)
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) acc[q] += ws[q * plane + (long long)s * C + c];
+  }
+  __shared__ float red[MAXPL][4][FCH];
+  const int wave = threadIdx.x / 64;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    float v = acc[q];
+    v += __shfl_xor(v, FCH, 64);
+    v += __shfl_xor(v, 2 * FCH, 64);
+    v += __shfl_xor(v, 4 * FCH, 64);
+    if ((threadIdx.x & 63) < FCH) red[q][wave][ch] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < npl * FCH) {
+    const int q = threadIdx.x / FCH;
+    tot[q][ch] = red[q][0][ch] + red[q][1][ch] + red[q][2][ch] + red[q][3][ch];
+  }
+  __syncthreads();
+}
+
+// ---- forward statistics -------------------------------------------------------------------
+// Sums shifted by a common per-channel value K = x[first row of the segment] (so partials are
+// plain sums and merge by addition): partial[seg][q][split][c], q = 0: sum(x-K), 1: sum((x-K)^2).
+// A block = CB chunk-columns x RPB rows; rows past P load K itself and contribute zero.
 template <class T>
 __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x, long long ld, int P,
                                                         int C, float* __restrict__ ws) {
@@ -40,120 +139,69 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
   const Layout L = layout_of<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
-  const bool act = chunk < L.CPR && ty < L.RPB;
-  float sh[V], s[V], ss[V];
-  int n = 0;
+  const int S = gridDim.y, seg = blockIdx.z;
+  const T* xs = x + (long long)seg * P * ld;
+  float s[V], ss[V];
 #pragma unroll
-  for (int v = 0; v < V; ++v) { sh[v] = 0.f; s[v] = 0.f; ss[v] = 0.f; }
-  if (act) {
-    const int step = gridDim.y * L.RPB;
-    for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
-      float f[UNR][V];
+  for (int v = 0; v < V; ++v) { s[v] = 0.f; ss[v] = 0.f; }
+  if (chunk < L.CPR && ty < L.RPB) {
+    float K[V];
+    ld_chunk(xs + chunk * V, K);
+    const int step = S * L.RPB;
+    for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += SUNR * step) {
+      float f[SUNR][V];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u)  // UNR independent 16-B loads in flight per thread
-        if (r0 + u * step < P) ld_chunk(x + (long long)(r0 + u * step) * ld + chunk * V, f[u]);
-      if (n == 0) {
+      for (int u = 0; u < SUNR; ++u) {  // SUNR independent 16-B loads in flight per thread
+        const int r = r0 + u * step;
+        if (r < P) ld_chunk(xs + (long long)r * ld + chunk * V, f[u]);
+        else {
 #pragma unroll
-        for (int v = 0; v < V; ++v) sh[v] = f[0][v];
+          for (int v = 0; v < V; ++v) f[u][v] = K[v];
+        }
       }
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        if (r0 + u * step >= P) break;
+      for (int u = 0; u < SUNR; ++u)
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-          float d = f[u][v] - sh[v];
+          float d = f[u][v] - K[v];
           s[v] += d;
           ss[v] = fmaf(d, d, ss[v]);
         }
-        ++n;
-      }
     }
   }
-  // per-thread (mean, M2)
-  __shared__ float lm[256 * 8], l2[256 * 8];
-  __shared__ int ln[256];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    float mean = n ? sh[v] + s[v] / n : 0.f;
-    float m2 = n ? fmaxf(ss[v] - s[v] * s[v] / n, 0.f) : 0.f;
-    lm[threadIdx.x * V + v] = mean;
-    l2[threadIdx.x * V + v] = m2;
-  }
-  ln[threadIdx.x] = n;
-  __syncthreads();
-  if (ty == 0 && chunk < L.CPR) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float cn = 0.f, cm = 0.f, c2 = 0.f;
-      for (int k = 0; k < L.RPB; ++k) {
-        int t = k * L.CB + tx;
-        float nb = (float)ln[t];
-        if (nb == 0.f) continue;
-        float mb = lm[t * V + v], m2b = l2[t * V + v];
-        float nn = cn + nb, d = mb - cm;
-        cm += d * nb / nn;
-        c2 += m2b + d * d * cn * nb / nn;
-        cn = nn;
-      }
-      long long o = ((long long)blockIdx.y * C + chunk * V + v) * 3;
-      ws[o] = cn; ws[o + 1] = cm; ws[o + 2] = c2;
-    }
-  }
+  block_col_sums<V, 2>(L, tx, ty, s, ss, nullptr, ws + (long long)seg * 2 * S * C, S, C);
 }
 
-// block = 64 channels x 16 split-lanes (1024 threads); each lane Chan-merges every 16th split
-// partial, then a 16-way merge through LDS.
-__global__ __launch_bounds__(1024) void bn_stats_finalize(const float* __restrict__ ws, int S, int C,
-                                                          float* mean, float* invstd, float* run_mean,
-                                                          float* run_var, float momentum, float eps) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane = threadIdx.x >> 6;
-  float cn = 0.f, cm = 0.f, c2 = 0.f;
-  if (c < C) {
-    // 4 partials loaded per round (independent loads in flight), then merged in order
-    for (int s0 = lane; s0 < S; s0 += 64) {
-      float pn[4], pm[4], pq[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int s = s0 + 16 * u;
-        const float* w = ws + ((long long)(s < S ? s : 0) * C + c) * 3;
-        pn[u] = s < S ? w[0] : 0.f;
-        pm[u] = w[1];
-        pq[u] = w[2];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pn[u] == 0.f) continue;
-        float nn = cn + pn[u], d = pm[u] - cm, r = pn[u] / nn;
-        cm = fmaf(d, r, cm);
-        c2 += pq[u] + d * d * cn * r;
-        cn = nn;
-      }
+// mean / invstd per segment; running stats updated segment after segment (the reference runs
+// the encoder once per frame, so each frame's batch is one BN call).
+template <class T, int NSEG>
+__global__ __launch_bounds__(256) void bn_stats_finalize(const float* __restrict__ ws, int S, int C,
+                                                         const T* __restrict__ x,
+                                                         long long ld, int P, float* mean,
+                                                         float* invstd, float* run_mean,
+                                                         float* run_var, float momentum, float eps) {
+  const int c0 = blockIdx.x * FCH;
+  __shared__ float tot[MAXPL][FCH];
+  plane_sums<2 * NSEG>(ws, S, C, c0, tot);
+  const int c = c0 + threadIdx.x;
+  if (threadIdx.x >= FCH || c >= C) return;
+  double rm = 0, rv = 0;
+  if (run_mean) { rm = run_mean[c]; rv = run_var[c]; }
+  for (int seg = 0; seg < NSEG; ++seg) {
+    const double n = P, K = tof(x[(long long)seg * P * ld + c]);
+    const double s1 = tot[2 * seg][threadIdx.x], s2 = tot[2 * seg + 1][threadIdx.x];
+    const double md = s1 / n;
+    const double q = s2 - s1 * md > 0 ? s2 - s1 * md : 0.0;  // sum of squared deviations
+    const double var = q / n;
+    mean[seg * C + c] = (float)(K + md);
+    invstd[seg * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+      const double unb = n > 1 ? q / (n - 1) : var;
+      rm = (float)((1.0 - momentum) * rm + momentum * (K + md));
+      rv = (float)((1.0 - momentum) * rv + momentum * unb);
     }
   }
-  __shared__ float sn[16][64], sm[16][64], s2[16][64];
-  sn[lane][threadIdx.x & 63] = cn;
-  sm[lane][threadIdx.x & 63] = cm;
-  s2[lane][threadIdx.x & 63] = c2;
-  __syncthreads();
-  if (lane != 0 || c >= C) return;
-  double n = 0, m = 0, q = 0;
-  for (int k = 0; k < 16; ++k) {
-    double nb = sn[k][threadIdx.x];
-    if (nb == 0) continue;
-    double nn = n + nb, d = sm[k][threadIdx.x] - m;
-    m += d * nb / nn;
-    q += s2[k][threadIdx.x] + d * d * n * nb / nn;
-    n = nn;
-  }
-  double var = n > 0 ? q / n : 0.0;
-  mean[c] = (float)m;
-  invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (run_mean) {
-    double unb = n > 1 ? q / (n - 1) : var;
-    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
-    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
-  }
+  if (run_mean) { run_mean[c] = (float)rm; run_var[c] = (float)rv; }
 }
 
 __global__ void bn_eval_params(const float* rm, const float* rv, int C, float eps, float* mean, float* invstd) {
@@ -163,7 +211,22 @@ __global__ void bn_eval_params(const float* rm, const float* rv, int C, float ep
   invstd[c] = 1.0f / sqrtf(rv[c] + eps);
 }
 
-// ---- apply: y = act(bn(x) [+ res | + bn_r(xr)]) -----------------------------------------
+// V consecutive fp32 per-channel constants (16-byte aligned; null -> dflt)
+template <int V>
+__device__ __forceinline__ void ld_params(const float* p, int c0, float dflt, float* o) {
+  if (!p) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) o[v] = dflt;
+    return;
+  }
+#pragma unroll
+  for (int v = 0; v < V; v += 4) {
+    f32x4 q = *(const f32x4*)(p + c0 + v);
+    o[v] = q[0]; o[v + 1] = q[1]; o[v + 2] = q[2]; o[v + 3] = q[3];
+  }
+}
+
+// ---- apply: y = act(bn(x) [+ res | + bn_r(xr)]) per segment (blockIdx.z) -------------------
 template <class T>
 __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long long ldx, int P, int C,
                                                   const float* mean, const float* invstd,
@@ -179,17 +242,27 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
   if (chunk >= L.CPR || ty >= L.RPB) return;
-  float sc[V], sf[V], rsc[V], rsf[V];
+  const int seg = blockIdx.z, c0 = chunk * V;
+  const long long row0 = (long long)seg * P;
+  float sc[V], sf[V], rsc[V], rsf[V], t0[V], t1[V];
+  ld_params<V>(gamma, c0, 1.f, sc);
+  ld_params<V>(beta, c0, 0.f, sf);
+  ld_params<V>(invstd + seg * C, c0, 1.f, t0);
+  ld_params<V>(mean + seg * C, c0, 0.f, t1);
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    int c = chunk * V + v;
-    float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    sc[v] = g * invstd[c];
-    sf[v] = b - mean[c] * sc[v];
-    if (xr) {
-      float rg = rgamma ? rgamma[c] : 1.f, rb = rbeta ? rbeta[c] : 0.f;
-      rsc[v] = rg * rinvstd[c];
-      rsf[v] = rb - rmean[c] * rsc[v];
+    sc[v] *= t0[v];
+    sf[v] -= t1[v] * sc[v];
+  }
+  if (xr) {
+    ld_params<V>(rgamma, c0, 1.f, rsc);
+    ld_params<V>(rbeta, c0, 0.f, rsf);
+    ld_params<V>(rinvstd + seg * C, c0, 1.f, t0);
+    ld_params<V>(rmean + seg * C, c0, 0.f, t1);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      rsc[v] *= t0[v];
+      rsf[v] -= t1[v] * rsc[v];
     }
   }
   const float a = (act == 2) ? prelu[0] : 0.f;
@@ -198,16 +271,16 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
     float f[UNR][V], q[UNR][V];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int r = r0 + u * step;
-      if (r >= P) break;
-      ld_chunk(x + (long long)r * ldx + chunk * V, f[u]);
-      if (res) ld_chunk(res + (long long)r * ldr + chunk * V, q[u]);
-      if (xr) ld_chunk(xr + (long long)r * ldxr + chunk * V, q[u]);
+      const long long r = row0 + r0 + u * step;
+      if (r0 + u * step >= P) break;
+      ld_chunk(x + r * ldx + c0, f[u]);
+      if (res) ld_chunk(res + r * ldr + c0, q[u]);
+      if (xr) ld_chunk(xr + r * ldxr + c0, q[u]);
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int r = r0 + u * step;
-      if (r >= P) break;
+      const long long r = row0 + r0 + u * step;
+      if (r0 + u * step >= P) break;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float t = fmaf(f[u][v], sc[v], sf[v]);
@@ -217,14 +290,14 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         else if (act == 2) t = t > 0.f ? t : a * t;
         f[u][v] = t;
       }
-      st_chunk(y + (long long)r * ldy + chunk * V, f[u]);
+      st_chunk(y + r * ldy + c0, f[u]);
     }
   }
 }
 
-// ---- backward reduce: sum(dz), sum(dz * xhat) [, sum(dy * pre * (pre<=0)) for PReLU] ------
+// ---- backward reduce: planes sum(dz), sum(dz * xhat) [, sum(dz * pre * (pre<=0)) PReLU] ----
 // dz = dy * mask, mask = (y > 0) for act 1, 1 for act 0, (pre > 0 ? 1 : a) for act 2.
-template <class T>
+template <class T, int NQ>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, long long ldx,
                                                        const T* __restrict__ dy, long long lddy,
                                                        const T* __restrict__ y, long long ldy,
@@ -237,14 +310,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
   const bool on = chunk < L.CPR && ty < L.RPB;
+  const int c0 = on ? chunk * V : 0;
   float s1[V], s2[V], s3[V], mu[V], is[V], g[V], b[V];
+  ld_params<V>(mean, c0, 0.f, mu);
+  ld_params<V>(invstd, c0, 1.f, is);
+  ld_params<V>(gamma, c0, 1.f, g);
+  ld_params<V>(beta, c0, 0.f, b);
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    s1[v] = s2[v] = s3[v] = 0.f;
-    int c = on ? chunk * V + v : 0;
-    mu[v] = mean[c]; is[v] = invstd[c];
-    g[v] = gamma ? gamma[c] : 1.f; b[v] = beta ? beta[c] : 0.f;
-  }
+  for (int v = 0; v < V; ++v) s1[v] = s2[v] = s3[v] = 0.f;
   const float a = (act == 2) ? prelu[0] : 0.f;
   if (on) {
     const int step = gridDim.y * L.RPB;
@@ -254,9 +327,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
       for (int u = 0; u < UNR; ++u) {
         const int r = r0 + u * step;
         if (r >= P) break;
-        ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
-        ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
-        if (act == 1) ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
+        ld_chunk(x + (long long)r * ldx + c0, xf[u]);
+        ld_chunk(dy + (long long)r * lddy + c0, d[u]);
+        if (act == 1) ld_chunk(y + (long long)r * ldy + c0, yf[u]);
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -265,7 +338,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
         for (int v = 0; v < V; ++v) {
           float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
           float xh = (xf[u][v] - mu[v]) * is[v];
-          if (act == 2) {
+          if (NQ > 2) {
             float pre = fmaf(xh, g[v], b[v]);
             if (pre <= 0.f) { s3[v] = fmaf(dd, pre, s3[v]); dd *= a; }
           }
@@ -275,60 +348,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
       }
     }
   }
-  __shared__ float r1[256 * 8], r2[256 * 8], r3[256 * 8];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    r1[threadIdx.x * V + v] = s1[v]; r2[threadIdx.x * V + v] = s2[v]; r3[threadIdx.x * V + v] = s3[v];
-  }
-  __syncthreads();
-  if (ty == 0 && chunk < L.CPR) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      for (int k = 0; k < L.RPB; ++k) {
-        int t = (k * L.CB + tx) * V + v;
-        a1 += r1[t]; a2 += r2[t]; a3 += r3[t];
-      }
-      long long o = ((long long)blockIdx.y * C + chunk * V + v) * 3;
-      ws[o] = a1; ws[o + 1] = a2; ws[o + 2] = a3;
-    }
-  }
+  block_col_sums<V, NQ>(L, tx, ty, s1, s2, s3, ws, gridDim.y, C);
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict__ ws, int S, int C,
-                                                        float* sum_dz, float* sum_dzxh,
-                                                        float* dprelu_c) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane = threadIdx.x >> 6;
-  float a = 0.f, b = 0.f, d = 0.f;
-  if (c < C) {
-    for (int s0 = lane; s0 < S; s0 += 64) {
-      float pa[4], pb[4], pd[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int s = s0 + 16 * u;
-        const float* w = ws + ((long long)(s < S ? s : 0) * C + c) * 3;
-        const bool ok = s < S;
-        pa[u] = ok ? w[0] : 0.f;
-        pb[u] = ok ? w[1] : 0.f;
-        pd[u] = ok ? w[2] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { a += pa[u]; b += pb[u]; d += pd[u]; }
-    }
-  }
-  __shared__ float ra[16][64], rb[16][64], rd[16][64];
-  ra[lane][threadIdx.x & 63] = a;
-  rb[lane][threadIdx.x & 63] = b;
-  rd[lane][threadIdx.x & 63] = d;
-  __syncthreads();
-  if (lane != 0 || c >= C) return;
-  const int t = threadIdx.x;
-  float A = 0.f, Bs = 0.f, D = 0.f;
-  for (int k = 0; k < 16; ++k) { A += ra[k][t]; Bs += rb[k][t]; D += rd[k][t]; }
-  sum_dz[c] = A;
-  sum_dzxh[c] = Bs;
-  if (dprelu_c) dprelu_c[c] = D;
+template <int NQ>
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__ ws, int S, int C,
+                                                       float* sum_dz, float* sum_dzxh,
+                                                       float* dprelu_c) {
+  const int c0 = blockIdx.x * FCH;
+  __shared__ float tot[MAXPL][FCH];
+  plane_sums<NQ>(ws, S, C, c0, tot);
+  const int c = c0 + threadIdx.x;
+  if (threadIdx.x >= FCH || c >= C) return;
+  sum_dz[c] = tot[0][threadIdx.x];
+  sum_dzxh[c] = tot[1][threadIdx.x];
+  if (NQ > 2) dprelu_c[c] = tot[NQ > 2 ? 2 : 0][threadIdx.x];
 }
 
 // dx = gamma*invstd*(dz - sum_dz/P - xhat*sum_dzxh/P);  dres = dz (optional)
@@ -350,14 +384,18 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   if (chunk >= L.CPR || ty >= L.RPB) return;
   float mu[V], is[V], k1[V], m1[V], m2[V], g[V], b[V];
   const float invP = 1.f / (float)P;
+  const int c0 = chunk * V;
+  ld_params<V>(mean, c0, 0.f, mu);
+  ld_params<V>(invstd, c0, 1.f, is);
+  ld_params<V>(gamma, c0, 1.f, g);
+  ld_params<V>(beta, c0, 0.f, b);
+  ld_params<V>(sum_dz, c0, 0.f, m1);
+  ld_params<V>(sum_dzxh, c0, 0.f, m2);
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    int c = chunk * V + v;
-    mu[v] = mean[c]; is[v] = invstd[c];
-    g[v] = gamma ? gamma[c] : 1.f; b[v] = beta ? beta[c] : 0.f;
     k1[v] = g[v] * is[v];
-    m1[v] = sum_dz[c] * invP;
-    m2[v] = sum_dzxh[c] * invP;
+    m1[v] *= invP;
+    m2[v] *= invP;
   }
   const float a = (act == 2) ? prelu[0] : 0.f;
   const int step = gridDim.y * L.RPB;
@@ -393,48 +431,79 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   }
 }
 
-// Row blocks for a launch: ~`blocks` blocks in total, each thread walking >= min_rows rows.
-// Reductions (stats, backward sums) use min_rows 8 so the split count stays small for the
-// finalize pass; pure streaming passes (apply) use 2 for more parallelism.
-template <class T> int grid_rows(int P, int C, int* gx, int min_rows = 8, int blocks = 1024) {
+// Row blocks for a launch: ~`blocks` blocks in total over gx x gy x nseg, each thread walking
+// >= min_rows rows.  Reductions use min_rows 8 (one statistics round) so the split count the
+// finalize has to sum stays small; streaming passes (apply) use UNR rows per thread.
+template <class T> int grid_rows(int P, int C, int* gx, int min_rows, int blocks, int nseg = 1) {
   Layout L = layout_of<T>(C);
   *gx = (L.CPR + L.CB - 1) / L.CB;
-  int want = (blocks + *gx - 1) / *gx;
+  int want = (blocks / nseg + *gx - 1) / *gx;
   int maxy = (P + min_rows * L.RPB - 1) / (min_rows * L.RPB);
   int gy = want < maxy ? want : maxy;
   return gy < 1 ? 1 : gy;
 }
 
-template <class T> int splits_for(int P, int C) {
-  int gx;
-  int gy = grid_rows<T>(P, C, &gx);
-  return gy;
+int g_tune[8] = {1024, SUNR, 2048, UNR, 1024, UNR, 2048, UNR};  // see cn_bn_set_tuning
+enum { T_ST_BLOCKS, T_ST_ROWS, T_AP_BLOCKS, T_AP_ROWS, T_BR_BLOCKS, T_BR_ROWS, T_BA_BLOCKS, T_BA_ROWS };
+
+template <class T> int stat_splits(int P, int C, int nseg, int* gx) {
+  return grid_rows<T>(P, C, gx, g_tune[T_ST_ROWS], g_tune[T_ST_BLOCKS], nseg);
 }
+template <class T> int bwd_splits(int P, int C, int* gx) {
+  return grid_rows<T>(P, C, gx, g_tune[T_BR_ROWS], g_tune[T_BR_BLOCKS]);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
-extern "C" size_t cn_bn_workspace_floats(int dtype, int P, int C) {
-  int S = dtype == DT_BF16 ? splits_for<bf16>(P, C) : splits_for<float>(P, C);
-  return (size_t)S * C * 3;
+extern "C" int cn_bn_set_tuning(int key, int value) {
+  if (key < 0 || key >= 8 || value < 1) return CN_ERR_SHAPE;
+  g_tune[key] = value;
+  return 0;
 }
 
-extern "C" int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int C, float* mean,
+extern "C" size_t cn_bn_workspace_floats(int dtype, int P, int C, int nseg) {
+  int gx, s_st, s_bw;
+  if (dtype == DT_BF16) { s_st = stat_splits<bf16>(P, C, nseg, &gx); s_bw = bwd_splits<bf16>(P, C, &gx); }
+  else { s_st = stat_splits<float>(P, C, nseg, &gx); s_bw = bwd_splits<float>(P, C, &gx); }
+  size_t a = (size_t)nseg * 2 * s_st, b = (size_t)3 * s_bw;
+  return (a > b ? a : b) * C;
+}
+
+template <class T>
+static int bn_stats_launch(const T* x, long long ldx, int P, int nseg, int C, float* mean,
                            float* invstd, float* run_mean, float* run_var, float momentum,
                            float eps, float* ws, hipStream_t st) {
-  if (C % (dtype == DT_BF16 ? 8 : 4) || ldx % (dtype == DT_BF16 ? 8 : 4)) return CN_ERR_ALIGN;
-  int gx, gy;
-  if (dtype == DT_BF16) {
-    gy = grid_rows<bf16>(P, C, &gx);
-    hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C, ws);
-  } else {
-    gy = grid_rows<float>(P, C, &gx);
-    hipLaunchKernelGGL(bn_stats_partial<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C, ws);
-  }
+  int gx, gy = stat_splits<T>(P, C, nseg, &gx);
+  hipLaunchKernelGGL(bn_stats_partial<T>, dim3(gx, gy, nseg), dim3(256), 0, st, x, ldx, P, C, ws);
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, ws, gy, C, mean,
-                     invstd, run_mean, run_var, momentum, eps);
+  const dim3 fin((C + FCH - 1) / FCH);
+#define CN_FIN(NS)                                                                                 \
+  hipLaunchKernelGGL((bn_stats_finalize<T, NS>), fin, dim3(256), 0, st, ws, gy, C, x, ldx, P, mean, \
+                     invstd, run_mean, run_var, momentum, eps)
+  switch (nseg) {
+    case 1: CN_FIN(1); break;
+    case 2: CN_FIN(2); break;
+    case 3: CN_FIN(3); break;
+    case 4: CN_FIN(4); break;
+    default: return CN_ERR_UNSUPPORTED;
+  }
+#undef CN_FIN
   CN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                           float* mean, float* invstd, float* run_mean, float* run_var,
+                           float momentum, float eps, float* ws, hipStream_t st) {
+  if (C % (dtype == DT_BF16 ? 8 : 4) || ldx % (dtype == DT_BF16 ? 8 : 4)) return CN_ERR_ALIGN;
+  if (P < 1 || nseg < 1) return CN_ERR_SHAPE;
+  if (dtype == DT_BF16)
+    return bn_stats_launch<bf16>((const bf16*)x, ldx, P, nseg, C, mean, invstd, run_mean, run_var,
+                                 momentum, eps, ws, st);
+  return bn_stats_launch<float>((const float*)x, ldx, P, nseg, C, mean, invstd, run_mean, run_var,
+                                momentum, eps, ws, st);
 }
 
 extern "C" int cn_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps,
@@ -444,24 +513,58 @@ extern "C" int cn_bn_eval_params(const float* run_mean, const float* run_var, in
   return 0;
 }
 
-extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C, const float* mean,
-                           const float* invstd, const float* gamma, const float* beta,
-                           const void* res, long long ldr, const void* xr, long long ldxr,
-                           const float* rmean, const float* rinvstd, const float* rgamma,
-                           const float* rbeta, int act, const float* prelu, void* y,
-                           long long ldy, hipStream_t st) {
+extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                           const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, const void* res, long long ldr, const void* xr,
+                           long long ldxr, const float* rmean, const float* rinvstd,
+                           const float* rgamma, const float* rbeta, int act, const float* prelu,
+                           void* y, long long ldy, hipStream_t st) {
+  const int vec = dtype == DT_BF16 ? 8 : 4;
+  if (C % vec || ldx % vec || ldy % vec || (res && ldr % vec) || (xr && ldxr % vec)) return CN_ERR_ALIGN;
+  if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
+      !aligned16(rmean) || !aligned16(rinvstd) || !aligned16(rgamma) || !aligned16(rbeta))
+    return CN_ERR_ALIGN;
+  if (P < 1 || nseg < 1) return CN_ERR_SHAPE;
   int gx, gy;
   if (dtype == DT_BF16) {
-    gy = grid_rows<bf16>(P, C, &gx, UNR, 2048);
-    hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
+    gy = grid_rows<bf16>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
+    hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy, nseg), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
                        rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy);
   } else {
-    gy = grid_rows<float>(P, C, &gx, UNR, 2048);
-    hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx, P, C,
+    gy = grid_rows<float>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
+    hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy, nseg), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
                        rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy);
   }
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+template <class T>
+static int bn_bwd_launch(const T* x, long long ldx, const T* dy, long long lddy, const T* y,
+                         long long ldy, int P, int C, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int act, const float* prelu,
+                         float* dgamma, float* dbeta, float* dprelu_c, T* dx, long long lddx,
+                         T* dres, long long lddres, float* ws, hipStream_t st) {
+  int gx, gy = bwd_splits<T>(P, C, &gx);
+  const dim3 fin((C + FCH - 1) / FCH);
+  if (act == 2) {
+    hipLaunchKernelGGL((bn_bwd_reduce_k<T, 3>), dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy,
+                       P, C, mean, invstd, gamma, beta, act, prelu, ws);
+    CN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_bwd_finalize<3>, fin, dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_reduce_k<T, 2>), dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy,
+                       P, C, mean, invstd, gamma, beta, act, prelu, ws);
+    CN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_bwd_finalize<2>, fin, dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
+  }
+  CN_CHECK_LAUNCH();
+  if (!dx) return 0;
+  gy = grid_rows<T>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
+  hipLaunchKernelGGL(bn_bwd_apply_k<T>, dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy, P, C,
+                     mean, invstd, gamma, beta, act, prelu, dbeta, dgamma, dx, lddx, dres, lddres);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -472,32 +575,19 @@ extern "C" int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy
                          const float* prelu, float* dgamma, float* dbeta, float* dprelu_c,
                          void* dx, long long lddx, void* dres, long long lddres, float* ws,
                          hipStream_t st) {
-  int gx, gy;
-  if (dtype == DT_BF16) {
-    gy = grid_rows<bf16>(P, C, &gx);
-    hipLaunchKernelGGL(bn_bwd_reduce_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
-                       (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,
-                       act, prelu, ws);
-  } else {
-    gy = grid_rows<float>(P, C, &gx);
-    hipLaunchKernelGGL(bn_bwd_reduce_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
-                       (const float*)dy, lddy, (const float*)y, ldy, P, C, mean, invstd, gamma,
-                       beta, act, prelu, ws);
-  }
-  CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
-  CN_CHECK_LAUNCH();
-  if (!dx) return 0;
-  gy = dtype == DT_BF16 ? grid_rows<bf16>(P, C, &gx, UNR, 2048) : grid_rows<float>(P, C, &gx, UNR, 2048);
-  if (dtype == DT_BF16) {
-    hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
-                       (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C, mean, invstd, gamma, beta,
-                       act, prelu, dbeta, dgamma, (bf16*)dx, lddx, (bf16*)dres, lddres);
-  } else {
-    hipLaunchKernelGGL(bn_bwd_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
-                       (const float*)dy, lddy, (const float*)y, ldy, P, C, mean, invstd, gamma,
-                       beta, act, prelu, dbeta, dgamma, (float*)dx, lddx, (float*)dres, lddres);
-  }
-  CN_CHECK_LAUNCH();
-  return 0;
+  const int vec = dtype == DT_BF16 ? 8 : 4;
+  if (C % vec || ldx % vec || lddy % vec || (y && ldy % vec) || (dx && lddx % vec) ||
+      (dres && lddres % vec))
+    return CN_ERR_ALIGN;
+  if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
+      !aligned16(dgamma) || !aligned16(dbeta))
+    return CN_ERR_ALIGN;
+  if (P < 1) return CN_ERR_SHAPE;
+  if (dtype == DT_BF16)
+    return bn_bwd_launch<bf16>((const bf16*)x, ldx, (const bf16*)dy, lddy, (const bf16*)y, ldy, P, C,
+                               mean, invstd, gamma, beta, act, prelu, dgamma, dbeta, dprelu_c,
+                               (bf16*)dx, lddx, (bf16*)dres, lddres, ws, st);
+  return bn_bwd_launch<float>((const float*)x, ldx, (const float*)dy, lddy, (const float*)y, ldy, P, C,
+                              mean, invstd, gamma, beta, act, prelu, dgamma, dbeta, dprelu_c,
+                              (float*)dx, lddx, (float*)dres, lddres, ws, st);
 }

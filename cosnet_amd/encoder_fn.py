@@ -22,23 +22,30 @@ F = torch.autograd.Function
 
 
 # ---- segment helpers -----------------------------------------------------------------------
+class SegStats:
+    """BN statistics of nseg stacked frame segments: mean / invstd [nseg*C]; [i] -> segment i."""
+
+    def __init__(self, stats, nseg, c):
+        self.mean, self.invstd = stats
+        self.nseg, self.c = nseg, c
+
+    def __len__(self):
+        return self.nseg
+
+    def __getitem__(self, i):
+        return ops.seg_of((self.mean, self.invstd), i, self.c)
+
+
 def seg_stats(x, bn, training, nseg):
-    """Per-segment (frame) BN statistics; running stats updated segment by segment."""
-    p = x.shape[0] // nseg
-    return [bn_stats(x[i * p:(i + 1) * p], bn, training) for i in range(nseg)]
+    """Per-segment (frame) BN statistics in one launch pair; running stats updated segment by
+    segment."""
+    return SegStats(bn_stats(x, bn, training, nseg=nseg), nseg, x.shape[1])
 
 
 def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
-    nseg = len(stats)
-    p = x.shape[0] // nseg
-    if out is None:
-        out = torch.empty_like(x)
-    for i in range(nseg):
-        s = slice(i * p, (i + 1) * p)
-        bn_apply(x[s], stats[i], bn, act=act, prelu=prelu, res=None if res is None else res[s],
-                 xr=None if xr is None else xr[s], rstats=None if rstats is None else rstats[i],
-                 rbn=rbn, out=out[s])
-    return out
+    return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
+                    rstats=None if rstats is None else (rstats.mean, rstats.invstd), rbn=rbn,
+                    out=out, nseg=stats.nseg)
 
 
 # ---- stem --------------------------------------------------------------------------------------

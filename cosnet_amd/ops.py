@@ -203,31 +203,44 @@ def _nsplit_eff(k, nsplit, dt):
 
 
 # ---- batch norm -------------------------------------------------------------------------------
-def _ws(dtype, p, c, device):
-    n = nv.query("cn_bn_workspace_floats", nv.dtype_code(dtype), p, c)
+def _ws(dtype, p, c, device, nseg=1):
+    n = nv.query("cn_bn_workspace_floats", nv.dtype_code(dtype), p, c, nseg)
     return torch.empty((max(int(n), 1),), dtype=torch.float32, device=device)
 
 
-def bn_stats(x, bn, training, count_update=True):
-    """Returns (mean, invstd) fp32 [C].  Train mode updates bn.running_* (momentum 0.1)."""
+def bn_stats(x, bn, training, nseg=1, count_update=True):
+    """(mean, invstd) fp32 [nseg*C] of x = nseg stacked segments of equal rows, each its own
+    BN batch (one reference BN call per frame).  Train mode updates bn.running_* once per
+    segment, in order (momentum 0.1 each)."""
     p, c = x.shape
-    mean = torch.empty((c,), dtype=torch.float32, device=x.device)
+    if p % nseg:
+        raise ValueError("rows %d not divisible into %d segments" % (p, nseg))
+    p //= nseg
+    mean = torch.empty((nseg * c,), dtype=torch.float32, device=x.device)
     invstd = torch.empty_like(mean)
     if training:
         if p <= 1:
             raise ValueError("Expected more than 1 value per channel when training, got input size "
                              "torch.Size([%d, %d, 1, 1])" % (p, c))
-        ws = _ws(x.dtype, p, c, x.device)
+        ws = _ws(x.dtype, p, c, x.device, nseg)
         mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
-        nv.call("cn_bn_stats", dtc(x), x.data_ptr(), ld(x), p, c, mean.data_ptr(), invstd.data_ptr(),
-                bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(mom), float(bn.eps),
-                ws.data_ptr(), nv.stream())
+        nv.call("cn_bn_stats", dtc(x), x.data_ptr(), ld(x), p, nseg, c, mean.data_ptr(),
+                invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(mom),
+                float(bn.eps), ws.data_ptr(), nv.stream())
         if count_update:
-            bn._cn_nbt = getattr(bn, "_cn_nbt", 0) + 1
+            bn._cn_nbt = getattr(bn, "_cn_nbt", 0) + nseg
     else:
         nv.call("cn_bn_eval_params", bn.running_mean.data_ptr(), bn.running_var.data_ptr(), c,
                 float(bn.eps), mean.data_ptr(), invstd.data_ptr(), nv.stream())
+        if nseg > 1:
+            mean[c:].view(nseg - 1, c).copy_(mean[:c].expand(nseg - 1, c))
+            invstd[c:].view(nseg - 1, c).copy_(invstd[:c].expand(nseg - 1, c))
     return mean, invstd
+
+
+def seg_of(stats, i, c):
+    """Statistics of segment i out of bn_stats(..., nseg)."""
+    return stats[0][i * c:(i + 1) * c], stats[1][i * c:(i + 1) * c]
 
 
 def _affine(bn):
@@ -236,15 +249,17 @@ def _affine(bn):
     return None, None
 
 
-def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
+def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None,
+             nseg=1):
+    """y = act(bn(x) [+ res] [+ rbn(xr)]) with per-segment statistics ([nseg*C] each)."""
     p, c = x.shape
     if out is None:
         out = torch.empty((p, c), dtype=x.dtype, device=x.device)
     g, b = _affine(bn)
     rg, rb = _affine(rbn) if rbn is not None else (None, None)
-    nv.call("cn_bn_apply", dtc(x), x.data_ptr(), ld(x), p, c, stats[0].data_ptr(), stats[1].data_ptr(),
-            nv.ptr(g), nv.ptr(b), nv.ptr(res), ld(res) if res is not None else 0, nv.ptr(xr),
-            ld(xr) if xr is not None else 0, nv.ptr(rstats[0] if rstats else None),
+    nv.call("cn_bn_apply", dtc(x), x.data_ptr(), ld(x), p // nseg, nseg, c, stats[0].data_ptr(),
+            stats[1].data_ptr(), nv.ptr(g), nv.ptr(b), nv.ptr(res), ld(res) if res is not None else 0,
+            nv.ptr(xr), ld(xr) if xr is not None else 0, nv.ptr(rstats[0] if rstats else None),
             nv.ptr(rstats[1] if rstats else None), nv.ptr(rg), nv.ptr(rb), act, nv.ptr(prelu),
             out.data_ptr(), ld(out), nv.stream())
     return out

@@ -67,18 +67,24 @@ int cn_gemm(int dtype, int layout_a, int layout_b, int M, int N, int K, int ka_l
             hipStream_t stream);
 
 /* ---- BatchNorm2d (train: batch stats + running update; eval: running stats) ---------- */
-size_t cn_bn_workspace_floats(int dtype, int P, int C);
-int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int C, float* mean, float* invstd,
-                float* run_mean, float* run_var, float momentum, float eps, float* ws,
-                hipStream_t stream);
+/* x holds nseg segments of P rows each (frames a and b of a siamese pair, each its own BN
+ * batch as in the reference's two encoder calls, rgbd_segmentation_RAA.py:143-148, 198-203);
+ * mean/invstd are [nseg][C]; running stats are updated segment after segment. */
+size_t cn_bn_workspace_floats(int dtype, int P, int C, int nseg);
+int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int nseg, int C, float* mean,
+                float* invstd, float* run_mean, float* run_var, float momentum, float eps,
+                float* ws, hipStream_t stream);
 int cn_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps, float* mean,
                       float* invstd, hipStream_t stream);
-/* y = act(gamma*(x-mean)*invstd + beta [+ res] [+ bn_r(xr)]); act 0 none, 1 ReLU, 2 PReLU */
-int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int C, const float* mean,
-                const float* invstd, const float* gamma, const float* beta, const void* res,
-                long long ldr, const void* xr, long long ldxr, const float* rmean,
-                const float* rinvstd, const float* rgamma, const float* rbeta, int act,
-                const float* prelu, void* y, long long ldy, hipStream_t stream);
+/* y = act(gamma*(x-mean)*invstd + beta [+ res] [+ bn_r(xr)]); act 0 none, 1 ReLU, 2 PReLU.
+ * Per-channel arrays must be 16-byte aligned. */
+int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                const float* mean, const float* invstd, const float* gamma, const float* beta,
+                const void* res, long long ldr, const void* xr, long long ldxr,
+                const float* rmean, const float* rinvstd, const float* rgamma, const float* rbeta,
+                int act, const float* prelu, void* y, long long ldy, hipStream_t stream);
+/* launch-shape knobs (blocks / rows per thread of each BN pass), for tuning only */
+int cn_bn_set_tuning(int key, int value);
 /* backward of cn_bn_apply w.r.t. x (train mode), masks fused; dres <- dz for the residual */
 int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy, long long lddy,
               const void* y, long long ldy, int P, int C, const float* mean, const float* invstd,

@@ -194,6 +194,55 @@ def test_batchnorm_residual_forms(cuda, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c", [8, 256, 384])
+def test_batchnorm_segments(cuda, dt, c):
+    """Two frames stacked in one [2P, C] buffer, one BN batch each (the reference's two encoder
+    calls): per-frame statistics, running stats updated frame a then frame b, and the
+    downsample-residual apply with per-frame statistics of both BNs."""
+    n, h, w = 2, 9, 11
+    xa = (rnd((n, c, h, w), dt, 30) + 3.0).to(dt).double()
+    xb = (rnd((n, c, h, w), dt, 31, scale=0.5) - 1.0).to(dt).double()
+    da, db = rnd((n, c, h, w), dt, 32), rnd((n, c, h, w), dt, 33, scale=2.0)
+    bn, bnd = _bn_mod(c, cuda, 34), _bn_mod(c, cuda, 35)
+    rm, rv = bn.running_mean.double().cpu().clone(), bn.running_var.double().cpu().clone()
+    cpu = lambda m: (m.weight.detach().double().cpu(), m.bias.detach().double().cpu())
+    ya = F.batch_norm(xa, rm, rv, *cpu(bn), True, 0.1, 1e-5)
+    yb = F.batch_norm(xb, rm, rv, *cpu(bn), True, 0.1, 1e-5)
+    ra = F.batch_norm(da, None, None, *cpu(bnd), True, 0.1, 1e-5)
+    rb = F.batch_norm(db, None, None, *cpu(bnd), True, 0.1, 1e-5)
+    x = torch.cat([nhwc(xa), nhwc(xb)]).to(dt).to(cuda).contiguous()
+    d = torch.cat([nhwc(da), nhwc(db)]).to(dt).to(cuda).contiguous()
+    st = ops.bn_stats(x, bn, True, nseg=2)
+    std = ops.bn_stats(d, bnd, True, nseg=2)
+    y = ops.bn_apply(x, st, bn, act=1, xr=d, rstats=std, rbn=bnd, nseg=2)
+    torch.cuda.synchronize()
+    p = n * h * w
+    close(nchw(y[:p], n, h, w), F.relu(ya + ra), dt)
+    close(nchw(y[p:], n, h, w), F.relu(yb + rb), dt)
+    close(bn.running_mean, rm, torch.float32, scale=1.0)
+    close(bn.running_var, rv, torch.float32, scale=1.0)
+    assert bn._cn_nbt == 2
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("pc", [(4 * 119 * 119, 64), (4 * 60 * 60, 1024)])
+def test_batchnorm_stats_large(cuda, dt, pc):
+    """Statistics at the step's sizes, with a channel mean far from zero (shifted sums)."""
+    p, c = pc
+    g = torch.Generator(device=cuda).manual_seed(36)
+    off = torch.linspace(-20, 20, c, device=cuda)
+    x = (torch.randn((p, c), generator=g, device=cuda) * 0.7 + off).to(dt)
+    bn = _bn_mod(c, cuda, 37)
+    mean, invstd = ops.bn_stats(x, bn, True)
+    xd = x.double()
+    m_ref = xd.mean(0)
+    v_ref = xd.var(0, unbiased=False)
+    torch.cuda.synchronize()
+    assert (mean.double() - m_ref).abs().max().item() <= 1e-5 * (1 + m_ref.abs().max().item())
+    assert ((invstd.double() - (v_ref + 1e-5).rsqrt()) / (v_ref + 1e-5).rsqrt()).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_bn_eval(cuda, dt):
     n, c, h, w = 1, 256, 4, 6
     x = rnd((n, c, h, w), dt, 17)
