@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     return ap.parse_args()
 
 
@@ -83,10 +84,10 @@ def main():
     dev = torch.device("cuda", local)
 
     import cosnet_amd as C
-    from cosnet_amd import loss as L
     from cosnet_amd import ops
     from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
     from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
+    from cosnet_amd.train_step import TrainStep
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(1234)
@@ -98,46 +99,43 @@ def main():
     model = model.to(dev).train()
     g0, g1 = reference_param_groups(model)
     opt = SGD([g0, g1], [0.0, 0.0], momentum=0.9, weight_decay=5e-4)
-    net = model
-    if world > 1:
-        net = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local], broadcast_buffers=True, bucket_cap_mb=64,
-            gradient_as_bucket_view=True)
 
     B, S = args.batch, args.size
-    ra, rb, da, db, ga, gb = [t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)]
+    step = TrainStep(model, opt, B, S, graphed=bool(args.graph))
+    step.load(*[t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)])
     max_iter = 10000
 
-    def step(i):
+    def lrs(i):
         lr = lr_poly(2.5e-4, i, max_iter, 0.9, 0)
-        opt.set_lrs([0.01 * lr, 10 * lr])           # train.py:171-172
-        opt.zero_grad()
-        x1, x2, _ = net(ra, rb, da, db)
-        loss = L.bce_l1(x1, ga) + L.bce_l1(x2, gb)
-        loss.backward()
-        opt.step()
-        return loss
+        return [0.01 * lr, 10 * lr]                  # train.py:171-172
 
     def log(msg):
         if rank == 0:
             print("[bench] " + msg, file=sys.stderr, flush=True)
 
-    for i in range(args.warmup):
+    # warmup: the first (eager) iterations happen inside capture(); the rest are replays
+    prof = ops.GemmProfile() if not args.no_roofline else None
+    t1 = time.perf_counter()
+    nw = max(1, min(args.warmup, 2))
+    opt.set_lrs(lrs(0))
+    step.capture(warmup=nw)
+    torch.cuda.synchronize()
+    log("capture + %d eager warmup steps: %.1f s" % (nw, time.perf_counter() - t1))
+    for i in range(nw, args.warmup):
         t1 = time.perf_counter()
-        step(i)
+        step(lrs(i))
         torch.cuda.synchronize()
         log("warmup step %d: %.1f ms" % (i, (time.perf_counter() - t1) * 1e3))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    prof = ops.GemmProfile() if not args.no_roofline else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if prof:
+    if prof and not args.graph:
         prof.__enter__()
     for i in range(args.steps):
-        loss = step(args.warmup + i)
-    if prof:
+        loss = step(lrs(args.warmup + i))
+    if prof and not args.graph:
         prof.__exit__()
     torch.cuda.synchronize()
     if world > 1:
@@ -168,8 +166,16 @@ def main():
                    "loss": float(loss.item())},
         "model_tflops_per_s": pairs * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
     }
+    if prof and args.graph:
+        # ROCm graphs cannot carry timing events: time the GEMM launches of one more step,
+        # run eagerly right after the timed replays (same kernels, shapes and weights)
+        with prof:
+            step.eager(lrs(args.warmup + args.steps))
+        torch.cuda.synchronize()
     if prof:
         n, fl, kt = prof.summary()
+        if args.graph:  # one eager step: scale to the timed steps
+            n, fl, kt = n * args.steps, fl * args.steps, kt * args.steps
         peak = MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else MFMA_F32_PEAK_TFLOPS
         ach = fl / kt / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv/bmm)",

@@ -62,6 +62,8 @@ def _prof_start(flops):
     p = GemmProfile.active
     if p is None:
         return None
+    if torch.cuda.is_current_stream_capturing():
+        return None  # ROCm has no timing event nodes in graphs: profile an eager step instead
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()

@@ -12,6 +12,7 @@ once per occurrence, in order (torch's for-loop SGD semantics).
 """
 import struct
 
+import numpy as np
 import torch
 
 from . import _native as nv
@@ -55,6 +56,23 @@ class SGD:
         self._table_key = None
         self._lr_dev = None
         self._lr_static = False
+        self._stage = []      # [(pinned host uint8, device uint8)] per table
+        self._stage_cap = []  # records each can hold
+        self._graph_stage = []  # staging owned by recorded graphs (kept alive, never reused)
+
+    def reserve(self, counts=None):
+        """Allocate the pinned / device staging of the SGD tables (records per launch)."""
+        if counts is None:
+            counts = [sum(len(g) for g in self.groups)]
+        dev = self.groups[0][0].device if self.groups[0] else self.groups[1][0].device
+        self._stage, self._stage_cap = [], []
+        for n in counts:
+            host = torch.empty((max(n, 1) * _REC.size,), dtype=torch.uint8).pin_memory()
+            self._stage.append((host, torch.empty_like(host, device=dev)))
+            self._stage_cap.append(max(n, 1))
+        self._table_key = None
+        if self._lr_dev is None:
+            self._lr_dev = torch.zeros((len(self.lrs),), dtype=torch.float32, device=dev)
 
     def zero_grad(self, set_to_none=True):
         for g in self.groups:
@@ -109,15 +127,30 @@ class SGD:
         key = tuple(tuple(b) for b in batches)
         if key != self._table_key:
             # device tables of SgdTensor records, staged through pinned memory so the copy is
-            # asynchronous and capturable; rebuilt only when a pointer / flag changes
+            # asynchronous and capturable; rebuilt only when a pointer / flag changes.  The
+            # pinned staging buffers are allocated once (reserve()) and rewritten in place, so
+            # a rebuild inside a HIP-graph capture allocates nothing on the host.
+            capturing = torch.cuda.is_current_stream_capturing()
+            if not capturing and self._tables:
+                torch.cuda.current_stream().synchronize()  # earlier copies out of the staging
+            need = [len(b) for b in batches]
+            if len(self._stage) < len(need) or any(c < n for c, n in zip(self._stage_cap, need)):
+                if capturing:
+                    raise RuntimeError("SGD.reserve() must size the tables before graph capture")
+                self.reserve(need)
             self._tables = []
-            for b in batches:
+            for i, b in enumerate(batches):
                 blob = b"".join(_REC.pack(*r) for r in b)
-                host = torch.frombuffer(bytearray(blob), dtype=torch.uint8).pin_memory()
-                devt = torch.empty_like(host, device=dev)
-                devt.copy_(host, non_blocking=True)
+                host, devt = self._stage[i]
+                host[:len(blob)].numpy()[:] = np.frombuffer(blob, dtype=np.uint8)
+                devt[:len(blob)].copy_(host[:len(blob)], non_blocking=True)
                 self._tables.append((host, devt, len(b)))
             self._table_key = key
+            if capturing:
+                # the recorded copy reads this staging at every replay: hand it to the graph
+                # and never rewrite it (a later eager rebuild reserves a fresh set)
+                self._graph_stage.append(self._stage)
+                self._stage, self._stage_cap = [], []
         for host, devt, nrec in self._tables:
             nv.call("cn_sgd", devt.data_ptr(), nrec, self._lr_dev.data_ptr(), self.weight_decay,
                     self.momentum, nv.stream())

@@ -1,0 +1,94 @@
+"""The HIP-graph replayed training step (cosnet_amd/train_step.py) against the eager step."""
+import pytest
+import torch
+
+import cosnet_amd as C
+from cosnet_amd import ops
+from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
+from cosnet_amd.train_step import TrainStep
+
+
+def _setup(cuda, dtype, graphed, b=2, s=65):
+    torch.manual_seed(0)
+    m = C.build_model(dtype)
+    m.load_state_dict(recipe_state_dict(m.state_dict()))
+    m.encoder.main_classifier.requires_grad_(False)
+    m = m.to(cuda).train()
+    g0, g1 = reference_param_groups(m)
+    opt = SGD([g0, g1], [0.0, 0.0])
+    st = TrainStep(m, opt, b, s, graphed=graphed)
+    st.load(*[t.to(cuda) for t in synthetic_inputs(b, s, s, seed=5)])
+    return m, st
+
+
+def _lrs(i):
+    lr = lr_poly(2.5e-4, i, 100, 0.9, 0)
+    return [0.01 * lr, 10 * lr]  # train.py:171-172
+
+
+def _bufs(st):
+    return [st.opt.state[id(p)]["momentum_buffer"] for p in st.params if id(p) in st.opt.state]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graph_step_matches_eager(cuda, dtype):
+    """Graph replays follow the eager trajectory: losses and every SGD momentum buffer (the
+    running sum of each parameter's gradients, so a gradient contribution missing from the
+    recording shows up) agree with an eager run, within the spread of two eager runs (a few
+    reductions use fp32 atomics, so eager runs are not bitwise repeatable)."""
+    runs = [_setup(cuda, dtype, graphed=g) for g in (False, False, True)]
+    for _, st in runs:
+        st.opt.set_lrs(_lrs(0))
+        st.capture(warmup=2)
+    losses = [[], [], []]
+    for i in range(2):
+        for r, (_, st) in enumerate(runs):
+            losses[r].append(float(st(_lrs(2 + i))))
+    torch.cuda.synchronize()
+    for i in range(2):
+        ee = abs(losses[0][i] - losses[1][i])
+        eg = abs(losses[0][i] - losses[2][i])
+        assert eg <= max(4 * ee, 1e-5 * abs(losses[0][i])), (i, losses)
+    b0, b1, b2 = (_bufs(st) for _, st in runs)
+    assert len(b0) == len(b2) > 300
+    for k, (x0, x1, x2) in enumerate(zip(b0, b1, b2)):
+        scale = max(x0.abs().max().item(), 1e-12)
+        ee = (x0 - x1).abs().max().item() / scale
+        eg = (x0 - x2).abs().max().item() / scale
+        assert eg <= max(4 * ee, 1e-4), (k, tuple(x0.shape), ee, eg)
+    sde, sdg = runs[0][0].state_dict(), runs[2][0].state_dict()
+    for k in sde:
+        if k.endswith("num_batches_tracked"):
+            assert int(sde[k]) == int(sdg[k]), k
+        elif k.endswith("running_mean") or k.endswith("running_var"):
+            assert torch.allclose(sde[k], sdg[k], rtol=1e-3, atol=1e-4), k
+    # the eager path must see the weights the replays produced (weight cache invalidated)
+    me, mg, sg = runs[0][0], runs[2][0], runs[2][1]
+    with torch.no_grad():
+        xe = me(sg.rgb_a, sg.rgb_b, sg.dep_a, sg.dep_b)[0]
+        xg = mg(sg.rgb_a, sg.rgb_b, sg.dep_a, sg.dep_b)[0]
+    assert (xe - xg).abs().max().item() <= 1e-3
+
+
+@pytest.mark.gpu
+def test_eager_after_graph_keeps_graph_tables(cuda):
+    """An eager step after recording must not disturb the recorded SGD tables."""
+    m1, s1 = _setup(cuda, torch.bfloat16, graphed=True)
+    m2, s2 = _setup(cuda, torch.bfloat16, graphed=True)
+    for st in (s1, s2):
+        st.opt.set_lrs(_lrs(0))
+        st.capture(warmup=1)
+    s1(_lrs(1))
+    s2(_lrs(1))
+    prof = ops.GemmProfile()
+    with prof:
+        s1.eager(_lrs(2))
+    s2.eager(_lrs(2))
+    l1 = float(s1(_lrs(3)))
+    l2 = float(s2(_lrs(3)))
+    torch.cuda.synchronize()
+    n, fl, t = prof.summary()
+    assert n > 100 and fl > 0 and 0 < t < 1.0
+    assert abs(l1 - l2) <= 1e-5 * abs(l1)
