@@ -43,11 +43,14 @@ _SIGS = {
     "cn_maxpool_fwd": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cn_maxpool_bwd": (_I, [_I, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cn_avgpool": (_I, [_I, _P, _L, _I, _I, _I, _F, _P, _P, _P]),
+    "cn_avgpool_workspace_floats": (_S, [_I, _I, _I, _I]),
     "cn_bcast_rows": (_I, [_I, _P, _I, _I, _I, _F, _P, _L, _I, _P]),
     "cn_gate_fwd": (_I, [_I, _P, _L, _I, _I, _P, _P, _P, _L, _P, _P]),
-    "cn_gate_bwd": (_I, [_I, _P, _L, _P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _P, _P]),
+    "cn_gate_bwd": (_I, [_I, _P, _L, _P, _L, _P, _I, _I, _P, _I, _P, _L, _P, _P, _P, _P]),
+    "cn_colpart_workspace_floats": (_S, [_I, _I]),
+    "cn_mean_rows": (_I, [_P, _I, _I, _P, _P]),
     "cn_head_fwd": (_I, [_I, _P, _L, _P, _L, _I, _I, _I, _P, _P, _P, _L, _P, _P]),
-    "cn_head_bwd": (_I, [_I, _P, _L, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P]),
+    "cn_head_bwd": (_I, [_I, _P, _L, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
     "cn_upsample_sigmoid": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cn_upsample_sigmoid_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "cn_count_ge": (_I, [_P, _L, _F, _P, _P]),
@@ -56,7 +59,7 @@ _SIGS = {
     "cn_bce_l1_devcount": (_I, [_P, _P, _L, _P, ctypes.c_double, _F, _P, _P, _P, _P]),
     "cn_sgd": (_I, [_P, _I, _P, _F, _F, _P]),
     "cn_rowdot": (_I, [_I, _P, _L, _P, _L, _I, _I, _P, _P]),
-    "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P]),
+    "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P, _P]),
     "cn_cast2d": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _I, _P]),
 }
 

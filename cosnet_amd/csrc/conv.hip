@@ -29,6 +29,14 @@ static ConvGeom make_geom(int N, int H, int W, int C, int OH, int OW, int KH, in
 
 static int vec_of(int dtype) { return dtype == DT_BF16 ? 8 : 4; }
 
+// zero-fill with 16-byte vector stores (a kernel, not a memset node, inside captured graphs)
+__global__ void zero16_k(u32x4* p, long long n16) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n16;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = z;
+}
+
 extern "C" int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                            const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
                            const float* bias, void* y, long long ldy, int OH, int OW,
@@ -76,8 +84,11 @@ extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, i
   // (unless accumulating into an existing gradient).
   if (!accumulate) {
     if (lddx != Cin) return CN_ERR_ALIGN;
-    size_t bytes = (size_t)N * H * W * Cin * (dtype == DT_BF16 ? 2 : 4);
-    if (hipMemsetAsync(dx, 0, bytes, st) != hipSuccess) return CN_ERR_HIP;
+    long long n16 = (long long)N * H * W * Cin / vec_of(dtype);
+    if (((long long)Cin % vec_of(dtype)) || ((uintptr_t)dx & 15)) return CN_ERR_ALIGN;
+    long long nb = (n16 + 255) / 256;
+    hipLaunchKernelGGL(zero16_k, dim3(nb < 4096 ? nb : 4096), dim3(256), 0, st, (u32x4*)dx, n16);
+    CN_CHECK_LAUNCH();
   }
   a.M = N * OH * OW;
   a.row_map = 1;

@@ -125,7 +125,9 @@ __global__ void maxpool_bwd_k(const T* __restrict__ dy, const unsigned char* __r
 }
 
 // ---- global average pool over HW per image: T [N*HW][C] (ld) -> T [N][C] --------------
-// grid (ceil(C/V/64), N, RS): block = 64 chunks x 4 row groups; fp32 partials -> ws [N][C]
+// grid (ceil(C/V/64), N, RS): block = 64 chunks x 4 row groups; each (row split z) writes its
+// fp32 partial to ws [z][N][C]; avgpool_final_k sums the RS partials in a fixed order, so the
+// result is deterministic and no zero-fill / atomics are needed (graph-capture friendly).
 template <class T>
 __global__ __launch_bounds__(256) void avgpool_partial_k(const T* __restrict__ x, long long ld, int HW,
                                                          int C, float* __restrict__ ws) {
@@ -151,18 +153,23 @@ __global__ __launch_bounds__(256) void avgpool_partial_k(const T* __restrict__ x
   for (int v = 0; v < V; ++v) red[rg][threadIdx.x & 63][v] = acc[v];
   __syncthreads();
   if (rg == 0 && cc * V < C) {
+    float* dst = ws + ((long long)blockIdx.z * gridDim.y + n) * C + cc * V;
 #pragma unroll
     for (int v = 0; v < V; ++v)
-      atomicAdd(ws + (long long)n * C + cc * V + v, red[0][threadIdx.x][v] + red[1][threadIdx.x][v] +
-                                                        red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
+      dst[v] = (red[0][threadIdx.x][v] + red[1][threadIdx.x][v]) +
+               (red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
   }
 }
 
 template <class T>
-__global__ void scale_cast_k(const float* __restrict__ ws, long long n, float scale, T* __restrict__ y) {
+__global__ void avgpool_final_k(const float* __restrict__ ws, int rs, long long n, float scale,
+                                T* __restrict__ y) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    y[i] = fromf<T>(ws[i] * scale);
+       i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < rs; ++z) s += ws[(long long)z * n + i];
+    y[i] = fromf<T>(s * scale);
+  }
 }
 
 // broadcast T [N][C] over HW rows into dst (ld); scale applied (1 for fwd, 1/HW for avgpool bwd)
@@ -223,13 +230,48 @@ __global__ void gate_fwd_k(const T* __restrict__ z, long long ldz, int P, int C,
 
 // dz = dout*m + (sum_c dout*z) * m(1-m) * g ;  dg += sum_p (.)*z ; dgb += sum_p (.)
 // one wave per row, rows grid-strided; dg / dgb reduced per block before one atomic each.
+// ---- deterministic column reductions ------------------------------------------------------
+// A 4-wave block whose lane l holds V column sums acc (columns l*V..l*V+V-1) and wave-0 lane 0 a
+// scalar accb writes them as ONE row of partials: ws[blockIdx.x][0..C) and
+// ws[gridDim.x * C + blockIdx.x] (the scalar); colreduce_k then sums the rows in block order.
+// Fixed-order sums: results are bitwise repeatable run to run (no float atomics).
+template <int V>
+__device__ __forceinline__ void block_partials(const float* acc, float accb, bool on, int C,
+                                               float* __restrict__ ws) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float red[4][64][8];
+  __shared__ float redb[4];
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[wave][lane][v] = acc[v];
+  if (lane == 0) redb[wave] = accb;
+  __syncthreads();
+  if (wave == 0 && on) {
+    float* dst = ws + (long long)blockIdx.x * C + lane * V;
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      dst[v] = (red[0][lane][v] + red[1][lane][v]) + (red[2][lane][v] + red[3][lane][v]);
+  }
+  if (threadIdx.x == 0)
+    ws[(long long)gridDim.x * C + blockIdx.x] = (redb[0] + redb[1]) + (redb[2] + redb[3]);
+}
+
+// out[c] = scale * sum_{b < nb} part[b * C + c]  (in block order)
+__global__ void colreduce_k(const float* __restrict__ part, int nb, int C, float scale,
+                            float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
+  out[c] = s * scale;
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void gate_bwd_k(const T* __restrict__ z, long long ldz,
                                                   const T* __restrict__ dout, long long lddo,
                                                   const float* __restrict__ mask, int P, int C,
                                                   const float* __restrict__ g, int through_mask,
                                                   T* __restrict__ dz, long long lddz,
-                                                  float* __restrict__ dg, float* __restrict__ dgb) {
+                                                  float* __restrict__ ws) {
   constexpr int V = VecOf<T>::N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int CPR = C / V;  // <= 64 (checked by the launcher)
@@ -266,17 +308,8 @@ __global__ __launch_bounds__(256) void gate_bwd_k(const T* __restrict__ z, long 
       stv(dz + (long long)row * lddz + lane * V, o);
     }
   }
-  if (!dg) return;
-  __shared__ float red[4][64][8];
-#pragma unroll
-  for (int v = 0; v < V; ++v) red[wave][lane][v] = acc[v];
-  __syncthreads();
-  if (wave == 0 && on) {
-#pragma unroll
-    for (int v = 0; v < V; ++v)
-      atomicAdd(dg + lane * V + v, red[0][lane][v] + red[1][lane][v] + red[2][lane][v] + red[3][lane][v]);
-  }
-  if (dgb && lane == 0) atomicAdd(dgb, accb);
+  if (!ws) return;
+  block_partials<V>(acc, accb, on, C, ws);
 }
 
 // ---- decoder head: zr = relu(a [+ b]) (stored if zout), logit = zr . w + bias ---------------
@@ -317,7 +350,7 @@ __global__ __launch_bounds__(256) void head_bwd_k(const T* __restrict__ z, long 
                                                   const float* __restrict__ dlogit, int P, int C,
                                                   int relu, const float* __restrict__ w,
                                                   T* __restrict__ dz, long long lddz,
-                                                  float* __restrict__ dw, float* __restrict__ db) {
+                                                  float* __restrict__ ws) {
   constexpr int V = VecOf<T>::N;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int CPR = C / V;  // <= 64 (checked by the launcher)
@@ -339,16 +372,8 @@ __global__ __launch_bounds__(256) void head_bwd_k(const T* __restrict__ z, long 
     }
     if (dz) stv(dz + (long long)row * lddz + lane * V, o);
   }
-  __shared__ float red[4][64][8];
-#pragma unroll
-  for (int v = 0; v < V; ++v) red[wave][lane][v] = acc[v];
-  __syncthreads();
-  if (dw && wave == 0 && on) {
-#pragma unroll
-    for (int v = 0; v < V; ++v)
-      atomicAdd(dw + lane * V + v, red[0][lane][v] + red[1][lane][v] + red[2][lane][v] + red[3][lane][v]);
-  }
-  if (db && lane == 0) atomicAdd(db, accb);
+  if (!ws) return;
+  block_partials<V>(acc, accb, on, C, ws);
 }
 
 // ---- bilinear upsample (align_corners=False, torch semantics) + sigmoid ----------------
@@ -425,6 +450,12 @@ __global__ void upsample_sigmoid_bwd_k(const float* __restrict__ dout, const flo
 }
 
 // ---- loss: r*BCE + 0.8*L1 (train.py:176-216), gradient fused --------------------------
+__global__ void zero_u64_k(unsigned long long* p, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0ull;
+}
+
 __global__ void count_ge_k(const float* __restrict__ gt, long long n, float thr, unsigned long long* cnt) {
   unsigned long long c = 0;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
@@ -521,7 +552,9 @@ __global__ void rowdot_k(const T* __restrict__ a, long long lda, const T* __rest
 
 // column sums of T [P][C] (ld) into fp32 [C] (atomic across row blocks)
 template <class T>
-__global__ void colsum_k(const T* __restrict__ x, long long ld, int P, int C, float* __restrict__ out) {
+__global__ void colsum_k(const T* __restrict__ x, long long ld, int P, int C, float* __restrict__ part) {
+  // grid (ceil(C/V/64), gy): block (x, y) sums rows y*4+rg, y*4+rg + 4*gy, ... of its columns
+  // into part[y][C] (fixed order; colreduce_k adds the gy rows)
   constexpr int V = VecOf<T>::N;
   int cc = blockIdx.x * 64 + (threadIdx.x & 63);
   int rg = threadIdx.x >> 6;
@@ -541,10 +574,11 @@ __global__ void colsum_k(const T* __restrict__ x, long long ld, int P, int C, fl
   for (int v = 0; v < V; ++v) red[rg][threadIdx.x & 63][v] = acc[v];
   __syncthreads();
   if (rg == 0 && cc * V < C) {
+    float* dst = part + (long long)blockIdx.y * C + cc * V;
 #pragma unroll
     for (int v = 0; v < V; ++v)
-      atomicAdd(out + cc * V + v, red[0][threadIdx.x][v] + red[1][threadIdx.x][v] +
-                                      red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
+      dst[v] = (red[0][threadIdx.x][v] + red[1][threadIdx.x][v]) +
+               (red[2][threadIdx.x][v] + red[3][threadIdx.x][v]);
   }
 }
 
@@ -616,14 +650,23 @@ extern "C" int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* ar
   return 0;
 }
 
-extern "C" int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C,
-                          float scale, void* y, float* ws, hipStream_t st) {
-  int V = dtype == DT_BF16 ? 8 : 4;
-  if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)N * C, st) != hipSuccess) return CN_ERR_HIP;
+static int avgpool_splits(int N, int HW, int C, int V) {
   int gx = (C / V + 63) / 64;
   int rs = (HW + 255) / 256;
   if (rs * gx * N > 1024) rs = 1024 / (gx * N);
-  if (rs < 1) rs = 1;
+  return rs < 1 ? 1 : rs;
+}
+
+extern "C" size_t cn_avgpool_workspace_floats(int dtype, int N, int HW, int C) {
+  return (size_t)avgpool_splits(N, HW, C, dtype == DT_BF16 ? 8 : 4) * N * C;
+}
+
+extern "C" int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C,
+                          float scale, void* y, float* ws, hipStream_t st) {
+  int V = dtype == DT_BF16 ? 8 : 4;
+  if (C % V) return CN_ERR_ALIGN;
+  int gx = (C / V + 63) / 64;
+  int rs = avgpool_splits(N, HW, C, V);
   dim3 grid(gx, N, rs);
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(avgpool_partial_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, HW, C, ws);
@@ -632,9 +675,9 @@ extern "C" int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW,
   CN_CHECK_LAUNCH();
   long long n = (long long)N * C;
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(scale_cast_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, ws, n, scale, (bf16*)y);
+    hipLaunchKernelGGL(avgpool_final_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, ws, rs, n, scale, (bf16*)y);
   else
-    hipLaunchKernelGGL(scale_cast_k<float>, dim3(nblocks(n)), dim3(256), 0, st, ws, n, scale, (float*)y);
+    hipLaunchKernelGGL(avgpool_final_k<float>, dim3(nblocks(n)), dim3(256), 0, st, ws, rs, n, scale, (float*)y);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -661,17 +704,44 @@ extern "C" int cn_gate_fwd(int dtype, const void* z, long long ldz, int P, int C
   return 0;
 }
 
-extern "C" int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
-                           const float* mask, int P, int C, const float* g, int through_mask,
-                           void* dz, long long lddz, float* dg, float* dgb, hipStream_t st) {
-  if (C / (dtype == DT_BF16 ? 8 : 4) > 64) return CN_ERR_UNSUPPORTED;
-  dim3 grid(nblocks(P, 4 * 16));
-  if (dtype == DT_BF16)
-    hipLaunchKernelGGL(gate_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, (const bf16*)dout, lddo, mask, P, C, g, through_mask, (bf16*)dz, lddz, dg, dgb);
-  else
-    hipLaunchKernelGGL(gate_bwd_k<float>, grid, dim3(256), 0, st, (const float*)z, ldz, (const float*)dout, lddo, mask, P, C, g, through_mask, (float*)dz, lddz, dg, dgb);
+static int rowpart_blocks(int P) { return nblocks(P, 4 * 16); }
+
+extern "C" size_t cn_colpart_workspace_floats(int P, int C) {
+  return (size_t)rowpart_blocks(P) * (size_t)(C + 1);
+}
+
+static int colreduce(const float* ws, int nb, int C, float* out, hipStream_t st) {
+  if (!out) return 0;
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 255) / 256), dim3(256), 0, st, ws, nb, C, 1.f, out);
   CN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t st) {
+  if (nrows < 1 || C < 1) return CN_ERR_SHAPE;
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 255) / 256), dim3(256), 0, st, x, nrows, C,
+                     1.f / (float)nrows, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
+                           const float* mask, int P, int C, const float* g, int through_mask,
+                           void* dz, long long lddz, float* dg, float* dgb, float* ws,
+                           hipStream_t st) {
+  if (C / (dtype == DT_BF16 ? 8 : 4) > 64) return CN_ERR_UNSUPPORTED;
+  if ((dg || dgb) && !ws) return CN_ERR_SHAPE;
+  int nb = rowpart_blocks(P);
+  float* w = (dg || dgb) ? ws : nullptr;
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(gate_bwd_k<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)z, ldz, (const bf16*)dout, lddo, mask, P, C, g, through_mask, (bf16*)dz, lddz, w);
+  else
+    hipLaunchKernelGGL(gate_bwd_k<float>, dim3(nb), dim3(256), 0, st, (const float*)z, ldz, (const float*)dout, lddo, mask, P, C, g, through_mask, (float*)dz, lddz, w);
+  CN_CHECK_LAUNCH();
+  if (!w) return 0;
+  int rc = colreduce(ws, nb, C, dg, st);
+  if (rc) return rc;
+  return colreduce(ws + (long long)nb * C, nb, 1, dgb, st);
 }
 
 extern "C" int cn_head_fwd(int dtype, const void* a, long long lda, const void* b, long long ldb,
@@ -688,15 +758,20 @@ extern "C" int cn_head_fwd(int dtype, const void* a, long long lda, const void* 
 
 extern "C" int cn_head_bwd(int dtype, const void* z, long long ldz, const float* dlogit, int P, int C,
                            int relu, const float* w, void* dz, long long lddz, float* dw, float* db,
-                           hipStream_t st) {
+                           float* ws, hipStream_t st) {
   if (C / (dtype == DT_BF16 ? 8 : 4) > 64) return CN_ERR_UNSUPPORTED;
-  dim3 grid(nblocks(P, 4 * 16));
+  if ((dw || db) && !ws) return CN_ERR_SHAPE;
+  int nb = rowpart_blocks(P);
+  float* wp = (dw || db) ? ws : nullptr;
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(head_bwd_k<bf16>, grid, dim3(256), 0, st, (const bf16*)z, ldz, dlogit, P, C, relu, w, (bf16*)dz, lddz, dw, db);
+    hipLaunchKernelGGL(head_bwd_k<bf16>, dim3(nb), dim3(256), 0, st, (const bf16*)z, ldz, dlogit, P, C, relu, w, (bf16*)dz, lddz, wp);
   else
-    hipLaunchKernelGGL(head_bwd_k<float>, grid, dim3(256), 0, st, (const float*)z, ldz, dlogit, P, C, relu, w, (float*)dz, lddz, dw, db);
+    hipLaunchKernelGGL(head_bwd_k<float>, dim3(nb), dim3(256), 0, st, (const float*)z, ldz, dlogit, P, C, relu, w, (float*)dz, lddz, wp);
   CN_CHECK_LAUNCH();
-  return 0;
+  if (!wp) return 0;
+  int rc = colreduce(ws, nb, C, dw, st);
+  if (rc) return rc;
+  return colreduce(ws + (long long)nb * C, nb, 1, db, st);
 }
 
 extern "C" int cn_upsample_sigmoid(const float* in, int N, int h, int w, int H, int W,
@@ -718,7 +793,8 @@ extern "C" int cn_upsample_sigmoid_bwd(const float* dout, const float* out, int 
 }
 
 extern "C" int cn_count_ge(const float* gt, long long n, float thr, unsigned long long* cnt, hipStream_t st) {
-  if (hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st) != hipSuccess) return CN_ERR_HIP;
+  hipLaunchKernelGGL(zero_u64_k, dim3(1), dim3(64), 0, st, cnt, 1ll);
+  CN_CHECK_LAUNCH();
   hipLaunchKernelGGL(count_ge_k, dim3(nblocks(n)), dim3(256), 0, st, gt, n, thr, cnt);
   CN_CHECK_LAUNCH();
   return 0;
@@ -768,18 +844,20 @@ extern "C" int cn_rowdot(int dtype, const void* a, long long lda, const void* b,
   return 0;
 }
 
-extern "C" int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
+extern "C" int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out, float* ws,
                          hipStream_t st) {
   int V = dtype == DT_BF16 ? 8 : 4;
+  if (C % V) return CN_ERR_ALIGN;
   int gx = (C / V + 63) / 64;
   int gy = (P + 63) / 64;
   if (gy > 256) gy = 256;
+  if (gy > rowpart_blocks(P)) gy = rowpart_blocks(P);  // fits cn_colpart_workspace_floats
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(colsum_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ld, P, C, out);
+    hipLaunchKernelGGL(colsum_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ld, P, C, ws);
   else
-    hipLaunchKernelGGL(colsum_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ld, P, C, out);
+    hipLaunchKernelGGL(colsum_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ld, P, C, ws);
   CN_CHECK_LAUNCH();
-  return 0;
+  return colreduce(ws, gy, C, out, st);
 }
 
 extern "C" int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C,

@@ -163,9 +163,7 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     dev = x.device
     cat = torch.empty((P, 2560), dtype=dt, device=dev)
     pool = torch.empty((n, 2048), dtype=dt, device=dev)
-    apws = torch.empty((n * 2048,), dtype=torch.float32, device=dev)
-    nv.call("cn_avgpool", ops.dtc(x), x.data_ptr(), ops.ld(x), n, hw, 2048, 1.0 / hw,
-            pool.data_ptr(), apws.data_ptr(), nv.stream())
+    ops.avgpool(x, n, hw, 1.0 / hw, pool)
     wcf, wct = WCACHE.get(mod.conv.weight, dt)
     cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=mod.conv.bias)
     stp = seg_stats(cp, mod.bn_x, tr, nseg)
@@ -221,9 +219,7 @@ def aspp_bwd(item, dout, grads):
         dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
                         accumulate=dx is not None)
     dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
-    apws = torch.empty((n * 512,), dtype=torch.float32, device=dout.device)
-    nv.call("cn_avgpool", ops.dtc(dcat), dcat.data_ptr(), ops.ld(dcat), n, hw, 512, 1.0,
-            dyp.data_ptr(), apws.data_ptr(), nv.stream())
+    ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
     dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp[0], mod.bn_x, act=1)
     grads[mod.conv.weight] = as_param_grad(conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1),
                                            mod.conv.weight)

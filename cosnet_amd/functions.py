@@ -159,9 +159,7 @@ class ASPPFn(F):
         dev = x.device
         cat = torch.empty((P, 2560), dtype=dt, device=dev)
         pool = torch.empty((n, 2048), dtype=dt, device=dev)
-        apws = torch.empty((n * 2048,), dtype=torch.float32, device=dev)
-        nv.call("cn_avgpool", ops.dtc(x), x.data_ptr(), ops.ld(x), n, hw, 2048, 1.0 / hw,
-                pool.data_ptr(), apws.data_ptr(), nv.stream())
+        ops.avgpool(x, n, hw, 1.0 / hw, pool)
         wcf, wct = WCACHE.get(wc, dt)
         cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=bc)
         stp = bn_stats(cp, mod.bn_x, tr)
@@ -220,9 +218,7 @@ class ASPPFn(F):
             grads.append((dwi, dbias, dgi, dbi))
         # image-pool branch: sum over HW of its cat slice
         dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
-        apws = torch.empty((n * 512,), dtype=torch.float32, device=dout.device)
-        nv.call("cn_avgpool", ops.dtc(dcat), dcat.data_ptr(), ops.ld(dcat), n, hw, 512, 1.0,
-                dyp.data_ptr(), apws.data_ptr(), nv.stream())
+        ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
         dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp, mod.bn_x, act=1)
         dwc = conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1)
         dbc = ops.colsum(dcp)
@@ -355,11 +351,12 @@ class GateCatFn(F):
         dt = z.dtype
         dz = torch.empty_like(z)
         through = not ctx.mask_const
-        dg = torch.zeros((c,), dtype=torch.float32, device=z.device) if through else None
-        dgb = torch.zeros((1,), dtype=torch.float32, device=z.device) if (through and ctx.has_gb) else None
+        dg = torch.empty((c,), dtype=torch.float32, device=z.device) if through else None
+        dgb = torch.empty((1,), dtype=torch.float32, device=z.device) if (through and ctx.has_gb) else None
+        ws = ops.colpart_ws(P, c, z.device) if through else None
         nv.call("cn_gate_bwd", nv.dtype_code(dt), z.data_ptr(), ops.ld(z), dout.data_ptr(),
                 ops.ld(dout), mask.data_ptr(), P, c, gflat.data_ptr(), int(through), dz.data_ptr(), c,
-                nv.ptr(dg), nv.ptr(dgb), nv.stream())
+                nv.ptr(dg), nv.ptr(dgb), nv.ptr(ws), nv.stream())
         dv = dout[:, c:] if ctx.needs_input_grad[1] else None
         if dg is not None:
             dg = dg.view(1, c, 1, 1)
@@ -437,12 +434,13 @@ class HeadFn(F):
         z, wflat = ctx.s
         P, c = z.shape
         dz = torch.empty_like(z)
-        dw = torch.zeros((c,), dtype=torch.float32, device=z.device)
-        db = torch.zeros((1,), dtype=torch.float32, device=z.device)
+        dw = torch.empty((c,), dtype=torch.float32, device=z.device)
+        db = torch.empty((1,), dtype=torch.float32, device=z.device)
         dlogit = dlogit.contiguous()
+        ws = ops.colpart_ws(P, c, z.device)
         nv.call("cn_head_bwd", nv.dtype_code(z.dtype), z.data_ptr(), c, dlogit.data_ptr(), P, c,
                 int(ctx.relu), wflat.data_ptr(), dz.data_ptr(), c, dw.data_ptr(), db.data_ptr(),
-                nv.stream())
+                ws.data_ptr(), nv.stream())
         return dz, (dz if ctx.has_b else None), dw.view(ctx.wshape), db, None
 
 

@@ -36,12 +36,9 @@ def multi_reference_x1(model, target, target_depth, searches, search_depths):
     x1, _ = model.head_nhwc(va_n, vb, da_n, db, geo, input_size)
     out = torch.empty((1, 1) + input_size, dtype=torch.float32, device=x1.device)
     hw = input_size[0] * input_size[1]
-    # mean over the N outputs: a [N][HW] -> [1][HW] column reduction, then 1/N scaling
-    acc = torch.zeros((hw,), dtype=torch.float32, device=x1.device)
-    nv.call("cn_colsum", nv.DT_F32, x1.data_ptr(), hw, n, hw, acc.data_ptr(), nv.stream())
-    nv.call("cn_cast2d", nv.DT_F32, nv.DT_F32, acc.data_ptr(), hw, 1, hw, out.data_ptr(), hw, 0,
-            nv.stream())
-    out.mul_(1.0 / n)
+    # mean over the N outputs: a fixed-order [N][HW] -> [HW] column reduction scaled by 1/N
+    x1 = x1.contiguous()
+    nv.call("cn_mean_rows", x1.data_ptr(), n, hw, out.data_ptr(), nv.stream())
     return out
 
 

@@ -57,8 +57,18 @@ class GemmProfile:
         t = sum(r[1].elapsed_time(r[2]) for r in self.rec) * 1e-3
         return len(self.rec), fl, t
 
+    def by_tag(self):
+        """{tag: [launches, FLOPs, seconds]} -- tag = (op, M, N, K) of each launch."""
+        out = {}
+        for fl, e0, e1, tag in self.rec:
+            r = out.setdefault(tag, [0, 0.0, 0.0])
+            r[0] += 1
+            r[1] += fl
+            r[2] += e0.elapsed_time(e1) * 1e-3
+        return out
 
-def _prof_start(flops):
+
+def _prof_start(flops, tag=None):
     p = GemmProfile.active
     if p is None:
         return None
@@ -67,7 +77,7 @@ def _prof_start(flops):
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    p.rec.append((flops, e0, e1))
+    p.rec.append((flops, e0, e1, tag))
     return e1
 
 
@@ -117,7 +127,7 @@ def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
     oh, ow = out_hw(h, w, k, stride, pad, dil)
     if out is None:
         out = torch.empty((n * oh * ow, cout), dtype=x.dtype, device=x.device)
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("fwd", n * oh * ow, cout, k * k * cin))
     nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
             stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
     _prof_end(ev)
@@ -128,7 +138,7 @@ def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accu
     cout = wt.shape[1] // (k * k)
     if out is None:
         out = torch.empty((n * h * w, cin), dtype=dy.dtype, device=dy.device)
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("dgrad%d" % stride, n * h * w, cin, k * k * cout))
     nv.call("cn_conv_dgrad", dtc(dy), dy.data_ptr(), ld(dy), n, oh, ow, cout, wt.data_ptr(), cin,
             k, k, stride, pad, dil, out.data_ptr(), ld(out), h, w, int(accumulate), nv.stream())
     _prof_end(ev)
@@ -141,7 +151,7 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
         dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
     nws = int(nv.query("cn_conv_wgrad_workspace_floats", dtc(x), n, oh, ow, cout, k, k, cin))
     ws = torch.empty((nws,), dtype=torch.float32, device=x.device) if nws else None
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("wgrad", cout, k * k * cin, n * oh * ow))
     nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
             ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.ptr(ws), nv.stream())
     _prof_end(ev)
@@ -156,10 +166,31 @@ def as_param_grad(dw_flat, weight):
     return dw_flat.view(co, kh, kw, ci).permute(0, 3, 1, 2)
 
 
+def colpart_ws(p, c, device):
+    """Workspace of the deterministic column reductions (colsum, gate / head backward)."""
+    n = int(nv.query("cn_colpart_workspace_floats", p, c))
+    return torch.empty((max(n, 1),), dtype=torch.float32, device=device)
+
+
 def colsum(x, out=None):
+    """fp32 [C] column sums of x [P, C] (bias gradients), fixed-order (bitwise repeatable)."""
     if out is None:
-        out = torch.zeros((x.shape[1],), dtype=torch.float32, device=x.device)
-    nv.call("cn_colsum", dtc(x), x.data_ptr(), ld(x), x.shape[0], x.shape[1], out.data_ptr(), nv.stream())
+        out = torch.empty((x.shape[1],), dtype=torch.float32, device=x.device)
+    ws = colpart_ws(x.shape[0], x.shape[1], x.device)
+    nv.call("cn_colsum", dtc(x), x.data_ptr(), ld(x), x.shape[0], x.shape[1], out.data_ptr(),
+            ws.data_ptr(), nv.stream())
+    return out
+
+
+def avgpool(x, n, hw, scale, out):
+    """out [n, C] = scale * sum over the hw rows of each image of x [n*hw, C] (C = out width);
+    deterministic fixed-order reduction of row-split partials (AdaptiveAvgPool2d(1),
+    deeplab/deeplabv3_encoder.py:57; and its backward with scale 1)."""
+    c = out.shape[1]
+    nws = int(nv.query("cn_avgpool_workspace_floats", dtc(x), n, hw, c))
+    ws = torch.empty((max(nws, 1),), dtype=torch.float32, device=x.device)
+    nv.call("cn_avgpool", dtc(x), x.data_ptr(), ld(x), n, hw, c, float(scale), out.data_ptr(),
+            ws.data_ptr(), nv.stream())
     return out
 
 
@@ -176,7 +207,8 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
         ldc = n
         c_bs = m * n
     c_f32 = int(out.dtype == torch.float32)
-    ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k))
+    ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k),
+                     ("gemm%d%d" % (layout_a, layout_b), batch * m, n, k))
     if nsplit > 1 and c_mode in (0, 1) and batch == 1 and c_f32 and ldc == n:
         # split-K into fp32 slabs + fixed-order reduction (no atomic contention)
         slab = m * n

@@ -147,6 +147,8 @@ class TrainStep:
             self._body()
         after = self._bn_counts()
         self._nbt_delta = {m: after[m] - before[m] for m in after if after[m] != before[m]}
+        for m, k in before.items():  # recording executed nothing: only replays count
+            m._cn_nbt = k
         torch.cuda.synchronize()
 
     def eager(self, lrs):

@@ -112,7 +112,8 @@ int cn_maxpool_bwd(int dtype, const void* dy, const unsigned char* argmax, int N
                    int C, int OH, int OW, int k, int s, int pad, void* dx, hipStream_t stream);
 /* AdaptiveAvgPool2d(1) + 1x1 upsample broadcast: deeplab/deeplabv3_encoder.py:57-61 */
 int cn_avgpool(int dtype, const void* x, long long ld, int N, int HW, int C, float scale, void* y,
-               float* ws /* N*C floats */, hipStream_t stream);
+               float* ws /* cn_avgpool_workspace_floats() */, hipStream_t stream);
+size_t cn_avgpool_workspace_floats(int dtype, int N, int HW, int C);
 int cn_bcast_rows(int dtype, const void* src, int N, int HW, int C, float scale, void* dst,
                   long long ld, int accumulate, hipStream_t stream);
 /* gate: rgbd_segmentation_RAA.py:177-184 (RGB, no bias), :228-235 (depth, bias) */
@@ -120,14 +121,19 @@ int cn_gate_fwd(int dtype, const void* z, long long ldz, int P, int C, const flo
                 const float* gb, void* out, long long ldo, float* mask, hipStream_t stream);
 int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long long lddo,
                 const float* mask, int P, int C, const float* g, int through_mask, void* dz,
-                long long lddz, float* dg, float* dgb, hipStream_t stream);
+                long long lddz, float* dg, float* dgb,
+                float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
+/* Mean of N stacked fp32 maps [N][C] -> [C] (N-reference average, test.py:287-305) */
+int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t stream);
+/* Workspace of the deterministic column reductions (gate/head backward, colsum). */
+size_t cn_colpart_workspace_floats(int P, int C);
 /* fusion + 1x1 classifier: rgbd_segmentation_RAA.py:251-261 ; deeplabv3_encoder.py:138 */
 int cn_head_fwd(int dtype, const void* a, long long lda, const void* b, long long ldb, int P,
                 int C, int relu, const float* w, const float* bias, void* zout, long long ldz,
                 float* logit, hipStream_t stream);
 int cn_head_bwd(int dtype, const void* z, long long ldz, const float* dlogit, int P, int C,
                 int relu, const float* w, void* dz, long long lddz, float* dw, float* db,
-                hipStream_t stream);
+                float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 /* F.upsample(bilinear, align_corners=False) + sigmoid: rgbd_segmentation_RAA.py:262-266 */
 int cn_upsample_sigmoid(const float* in, int N, int h, int w, int H, int W, int apply_sigmoid,
                         float* out, hipStream_t stream);
@@ -148,7 +154,8 @@ int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float moment
            hipStream_t stream);
 int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb, int P, int C,
               float* out, hipStream_t stream);
-int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out, hipStream_t stream);
+int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
+              float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C, void* y,
               long long ldy, int accumulate, hipStream_t stream);
 
