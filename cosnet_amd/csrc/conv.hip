@@ -8,6 +8,7 @@ static GemmArgs gemm_defaults() {
   a.nsplit = 1;
   a.k_chunk = 1 << 30;
   a.alpha = 1.f;
+  a.cfg = -1;
   FastDiv one = fastdiv_make(1);
   a.ga.div_C = a.ga.div_KW = a.ga.div_OW = a.ga.div_OHW = one;
   a.gb = a.ga;
@@ -98,23 +99,31 @@ extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, i
   return cn_gemm_dispatch(a, dtype, 0, L_KC_DENSE, L_KC_DENSE, 1, st);
 }
 
-static int pick_splits(long long tiles, int K, int BK) {
-  // ~512 blocks (2 per CU) but every split keeps >= 8 K-tiles of work
-  long long want = (512 + tiles - 1) / tiles;
+
+// Weight-gradient plan: tile configuration and K split (M = Cout, N = KH*KW*Cin, K = pixels).
+// 256x256 tiles for the big ASPP-sized products, else 128x128 with 8 waves (128x64 for the
+// fp32 parity path); enough K splits to give ~2 blocks per CU (1 for the 256x256 tile, which
+// fills a CU's LDS), each split keeping >= 8 K tiles.
+static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
+                       int* chunk, int* cfg) {
+  int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
+  int BK = 8 * vec_of(dtype);
+  long long tiles;
+  int target = 512;
+  if (dtype == DT_BF16) {
+    *cfg = (M >= 256 && NN >= 4096) ? 10 : 11;
+    if (*cfg == 10) target = 256;
+    tiles = cn_gemm_cfg_blocks(*cfg, M, NN);
+  } else {
+    *cfg = -1;
+    tiles = (long long)((M + 127) / 128) * ((NN + 63) / 64);
+  }
+  long long want = (target + tiles - 1) / tiles;
   long long maxs = K / (8 * BK);
   if (maxs < 1) maxs = 1;
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
-  return (int)want;
-}
-
-static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
-                       int* chunk) {
-  int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
-  int BK = 8 * vec_of(dtype);
-  long long t128 = (long long)((M + 127) / 128) * ((NN + 127) / 128);
-  long long tiles = (NN <= 64 || t128 < 384) ? (long long)((M + 127) / 128) * ((NN + 63) / 64) : t128;
-  int ns = pick_splits(tiles, K, BK);
+  int ns = (int)want;
   int ch = (K + ns - 1) / ns;
   ch = (ch + BK - 1) / BK * BK;
   *nsplit = (K + ch - 1) / ch;
@@ -123,8 +132,8 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
 
 extern "C" size_t cn_conv_wgrad_workspace_floats(int dtype, int N, int OH, int OW, int Cout, int KH,
                                                  int KW, int Cin) {
-  int ns, ch;
-  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch);
+  int ns, ch, cfg;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg);
   return ns > 1 ? (size_t)ns * Cout * KH * KW * Cin : 0;
 }
 
@@ -144,8 +153,9 @@ extern "C" int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int
     lb = L_MC_CONV;
     a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
   }
-  int ns, ch;
-  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch);
+  int ns, ch, cfg;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg);
+  a.cfg = cfg;
   a.nsplit = ns;
   a.k_chunk = ch;
   if (ns == 1) {  // whole K in one block: write dw directly

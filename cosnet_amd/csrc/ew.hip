@@ -255,14 +255,28 @@ __device__ __forceinline__ void block_partials(const float* acc, float accb, boo
     ws[(long long)gridDim.x * C + blockIdx.x] = (redb[0] + redb[1]) + (redb[2] + redb[3]);
 }
 
-// out[c] = scale * sum_{b < nb} part[b * C + c]  (in block order)
-__global__ void colreduce_k(const float* __restrict__ part, int nb, int C, float scale,
-                            float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
-  out[c] = s * scale;
+// out[c] = scale * sum_{b < nb} part[b * C + c].  Block = 64 columns x 4 row groups; row group
+// w sums rows w, w+4, ... (4 loads in flight per step), then the 4 group sums are added in a
+// fixed order: deterministic.
+__global__ __launch_bounds__(256) void colreduce_k(const float* __restrict__ part, int nb, int C,
+                                                   float scale, float* __restrict__ out) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < C) {
+    int b = w;
+    for (; b + 12 < nb; b += 16) {
+      s0 += part[(long long)b * C + c];
+      s1 += part[(long long)(b + 4) * C + c];
+      s2 += part[(long long)(b + 8) * C + c];
+      s3 += part[(long long)(b + 12) * C + c];
+    }
+    for (; b < nb; b += 4) s0 += part[(long long)b * C + c];
+  }
+  __shared__ float red[4][64];
+  red[w][l] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (w == 0 && c < C) out[c] = ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) * scale;
 }
 
 template <class T>
@@ -712,14 +726,14 @@ extern "C" size_t cn_colpart_workspace_floats(int P, int C) {
 
 static int colreduce(const float* ws, int nb, int C, float* out, hipStream_t st) {
   if (!out) return 0;
-  hipLaunchKernelGGL(colreduce_k, dim3((C + 255) / 256), dim3(256), 0, st, ws, nb, C, 1.f, out);
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, ws, nb, C, 1.f, out);
   CN_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t st) {
   if (nrows < 1 || C < 1) return CN_ERR_SHAPE;
-  hipLaunchKernelGGL(colreduce_k, dim3((C + 255) / 256), dim3(256), 0, st, x, nrows, C,
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, x, nrows, C,
                      1.f / (float)nrows, out);
   CN_CHECK_LAUNCH();
   return 0;

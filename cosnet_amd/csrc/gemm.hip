@@ -21,8 +21,6 @@
 
 namespace {
 
-constexpr int NT = 256;
-
 template <class T> struct Frag;
 template <> struct Frag<bf16> { typedef bf16x8 type; };
 template <> struct Frag<float> { typedef f32x4 type; };
@@ -42,12 +40,15 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 }
 
 // -------------------------------------------------------------------------------------
-// Operand loader.  ROWS = BM (A) or BN (B).  Fills `ROWS/32` 16-byte chunks per thread.
+// Operand loader.  ROWS = BM (A) or BN (B); NT threads.  Fills ROWS*8/NT 16-byte chunks per
+// thread per K tile (a tile is ROWS x 128 bytes of k).
 // -------------------------------------------------------------------------------------
-template <class T, int ROWS, int KIND> struct Loader {
+template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr int VEC = VecOf<T>::N;
   static constexpr int BK = 8 * VEC;
-  static constexpr int NCH = ROWS / 32;           // chunks per thread
+  static constexpr int NCH = ROWS * 8 / NT;       // chunks per thread
+  static constexpr int RSTEP = NT / 8;            // KC: rows between a thread's chunks
+  static_assert(NCH >= 1 && NCH * NT == ROWS * 8, "tile rows must fill whole chunk rounds");
   static constexpr bool MC = (KIND == L_MC_DENSE || KIND == L_MC_CONV);
   static constexpr int CPR = ROWS / VEC;          // MC: chunks per k-row
   static constexpr int KROW_STEP = NT / CPR;      // MC: k-rows between a thread's chunks
@@ -70,7 +71,7 @@ template <class T, int ROWS, int KIND> struct Loader {
       g = geo;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        int row = origin + (tid >> 3) + 32 * i;
+        int row = origin + (tid >> 3) + RSTEP * i;
         int rr = row < lim ? row : 0;
         int q, rem, oy, ox;
         fdivmod(rr, g.div_OHW, q, rem);
@@ -99,7 +100,7 @@ template <class T, int ROWS, int KIND> struct Loader {
       int k = k0 + (tid & 7) * VEC;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        int row = origin + (tid >> 3) + 32 * i;
+        int row = origin + (tid >> 3) + RSTEP * i;
         bool ok = row < lim && k < klim;
         v[i] = ok ? *(const u32x4*)(base + (long long)row * ld + k) : zero;
       }
@@ -153,9 +154,9 @@ template <class T, int ROWS, int KIND> struct Loader {
       if (KIND == L_KC_DENSE) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) {
-          int row = origin + (tid >> 3) + 32 * i;
+          int row = origin + (tid >> 3) + RSTEP * i;
           bool ok = row < lim && k < klim;
-          glds16(ok ? (const void*)(base + (long long)row * ld + k) : zp, wbase + i * 4096);
+          glds16(ok ? (const void*)(base + (long long)row * ld + k) : zp, wbase + i * NT * 16);
         }
       } else {  // L_KC_CONV
         int tap, cc, r, ss;
@@ -167,7 +168,7 @@ template <class T, int ROWS, int KIND> struct Loader {
           int y = by[i] + oy, x = bx[i] + ox;
           bool ok = img[i] >= 0 && k < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
           long long pix = ((long long)img[i] * g.H + y) * g.W + x;
-          glds16(ok ? (const void*)(base + pix * ld + cc) : zp, wbase + i * 4096);
+          glds16(ok ? (const void*)(base + pix * ld + cc) : zp, wbase + i * NT * 16);
         }
       }
     } else {
@@ -195,7 +196,7 @@ template <class T, int ROWS, int KIND> struct Loader {
           if (col < lim && kr < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
             src = base + (((long long)im * g.H + y) * g.W + x) * ld + cic;
         }
-        glds16(src, wbase + i * 4096);
+        glds16(src, wbase + i * NT * 16);
       }
     }
   }
@@ -205,7 +206,7 @@ template <class T, int ROWS, int KIND> struct Loader {
     if (!MC) {
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        int row = (tid >> 3) + 32 * i, c = tid & 7;
+        int row = (tid >> 3) + RSTEP * i, c = tid & 7;
         *(u32x4*)(lds + row * 128 + ((c ^ (row & 7)) << 4)) = v[i];
       }
     } else {
@@ -278,19 +279,50 @@ template <> __device__ __forceinline__ void store_c<bf16>(bf16* c, float v, int 
 
 }  // namespace
 
-template <class T, class CT, int BM, int BN, int LA, int LB>
-__global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
+// Counted wait on this wave's vector-memory queue: all but the n*G youngest LDS-DMA chunks
+// have landed (n = tiles left in flight, G = chunks per thread per tile; immediates only).
+template <int G>
+__device__ __forceinline__ void wait_tiles(int n) {
+  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(G) : "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * G) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * G) : "memory");
+}
+
+// Workgroup barrier that does NOT drain the LDS-DMA queue (unlike __syncthreads(), whose
+// fence emits vmcnt(0)); the asm memory clobbers keep the compiler from moving LDS accesses
+// across it.
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------
+// The kernel.  Tile BM x BN, WM x WN waves (each a (BM/WM) x (BN/WN) block of 16x16 MFMA
+// tiles), S-deep ring of LDS stages filled by LDS-DMA: the DMA of tile kt+S-1 is issued while
+// tile kt is consumed, and each K step ends with a COUNTED wait for tile kt+1 only (the
+// younger S-2 tiles stay in flight across the barrier) -- one barrier per K step.
+// ---------------------------------------------------------------------------------------
+template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
+  constexpr int NT = WM * WN * 64;
   constexpr int VEC = VecOf<T>::N;
   constexpr int BK = 8 * VEC;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
   constexpr int STAGE = ABYTES + BBYTES;
-  constexpr int RM = BM / 32, RN = BN / 32;  // 16x16 blocks per wave in m / n
+  constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
+  constexpr int RM = TM / 16, RN = TN / 16;  // 16x16 blocks per wave in m / n
   constexpr bool AMC = (LA == L_MC_DENSE || LA == L_MC_CONV);
   constexpr bool BMC = (LB == L_MC_DENSE || LB == L_MC_CONV);
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  typedef Loader<T, BM, LA, NT> LdA;
+  typedef Loader<T, BN, LB, NT> LdB;
+  constexpr int G = LdA::NCH + LdB::NCH;
+  static_assert(S >= 2 && S <= 4, "2..4 stages");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   // XCD-aware tile order (guide §5.5 T1, bijective form): blocks are dealt round-robin over
   // the 8 XCDs, so remap the linear id to give every XCD a contiguous run of M-tiles that
   // share the same B (weight) panel in its private L2.
@@ -316,8 +348,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
   const T* Abase = (const T*)p.A + (long long)batch * p.a_bs;
   const T* Bbase = (const T*)p.B + (long long)batch * p.b_bs;
 
-  Loader<T, BM, LA> la;
-  Loader<T, BN, LB> lb;
+  LdA la;
+  LdB lb;
   la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid);
   lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid);
 
@@ -327,19 +359,24 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (nt > 0) {
-    la.issue(kbeg, m0, tid, smem);
-    lb.issue(kbeg, n0, tid, smem + ABYTES);
+  // prologue: tiles 0 .. S-2 in flight, wait for tile 0
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) {
+    if (s < nt) {
+      la.issue(kbeg + s * BK, m0, tid, smem + s * STAGE);
+      lb.issue(kbeg + s * BK, n0, tid, smem + s * STAGE + ABYTES);
+    }
   }
-  __syncthreads();  // vmcnt(0) + barrier: tile 0 landed for every wave
+  wait_tiles<G>(min(nt - 1, S - 2));
+  raw_barrier();
 
+  int cur = 0;                     // stage of tile kt
+  int nxt = S - 1;                 // stage of tile kt + S - 1
   for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nt;
-    if (more) {  // DMA the next tile into the other buffer while this one is consumed
-      char* nxt = smem + (cur ^ 1) * STAGE;
-      la.issue(kbeg + (kt + 1) * BK, m0, tid, nxt);
-      lb.issue(kbeg + (kt + 1) * BK, n0, tid, nxt + ABYTES);
+    if (kt + S - 1 < nt) {  // refill the stage consumed at kt-1 (all waves passed its barrier)
+      char* dst = smem + nxt * STAGE;
+      la.issue(kbeg + (kt + S - 1) * BK, m0, tid, dst);
+      lb.issue(kbeg + (kt + S - 1) * BK, n0, tid, dst + ABYTES);
     }
     const char* As = smem + cur * STAGE;
     const char* Bs = As + ABYTES;
@@ -348,9 +385,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
       if constexpr (sizeof(T) == 2) {
         bf16x8 af[RM], bfr[RN];
 #pragma unroll
-        for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, AMC>(As, wm * (BM / 2) + i * 16, pc, lane);
+        for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, AMC>(As, wm * TM + i * 16, pc, lane);
 #pragma unroll
-        for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, BMC>(Bs, wn * (BN / 2) + j * 16, pc, lane);
+        for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, BMC>(Bs, wn * TN + j * 16, pc, lane);
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
@@ -360,61 +397,71 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
         f32x4 af[RM], bfr[RN];
         if (!AMC) {
 #pragma unroll
-          for (int i = 0; i < RM; ++i) af[i] = read_frag_f32_kc<BM>(As, wm * (BM / 2) + i * 16, pc, lane);
+          for (int i = 0; i < RM; ++i) af[i] = read_frag_f32_kc<BM>(As, wm * TM + i * 16, pc, lane);
         } else {
 #pragma unroll
           for (int i = 0; i < RM; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) af[i][j] = read_frag_f32_mc<BM>(As, wm * (BM / 2) + i * 16, pc, j, lane);
+            for (int j = 0; j < 4; ++j) af[i][j] = read_frag_f32_mc<BM>(As, wm * TM + i * 16, pc, j, lane);
         }
         if (!BMC) {
 #pragma unroll
-          for (int i = 0; i < RN; ++i) bfr[i] = read_frag_f32_kc<BN>(Bs, wn * (BN / 2) + i * 16, pc, lane);
+          for (int i = 0; i < RN; ++i) bfr[i] = read_frag_f32_kc<BN>(Bs, wn * TN + i * 16, pc, lane);
         } else {
 #pragma unroll
           for (int i = 0; i < RN; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[i][j] = read_frag_f32_mc<BN>(Bs, wn * (BN / 2) + i * 16, pc, j, lane);
+            for (int j = 0; j < 4; ++j) bfr[i][j] = read_frag_f32_mc<BN>(Bs, wn * TN + i * 16, pc, j, lane);
         }
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
           for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int j = 0; j < RN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s4], bfr[j][s4], acc[i][j], 0, 0, 0);
       }
     }
-    __syncthreads();  // drains this wave's DMA (vmcnt(0)) and orders it for all readers
+    // tile kt+1 must have landed (for every wave: counted wait, then the barrier); the
+    // min(nt-1, kt+S-1) - (kt+1) younger tiles stay in flight
+    wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
+    raw_barrier();
+    cur = cur + 1 == S ? 0 : cur + 1;
+    nxt = nxt + 1 == S ? 0 : nxt + 1;
   }
 
-  // Epilogue: stage alpha*acc (fp32) through LDS as [BM/2][BN+4] one wave-row half at a time,
-  // then every thread writes 8 consecutive columns of a row (16-B bf16 / 2x16-B fp32 stores,
-  // or 8 contiguous atomics).  Lane holds C[4g + r][l & 15] of each 16x16 block.
+  // Epilogue: stage alpha*acc (fp32) through LDS, HR tile rows per pass, as [HR][BN+4]; then
+  // every thread writes 8 consecutive columns of a row (16-B bf16 / 2x16-B fp32 stores, or 8
+  // contiguous atomics).  Lane holds C[4g + r][l & 15] of each 16x16 block.
   constexpr int LDC = BN + 4;
-  constexpr int HR = BM / 2;
-  static_assert(HR * LDC * 4 <= 2 * STAGE, "epilogue staging must fit in the LDS image");
+  constexpr int HR = (BM * LDC * 4 <= S * STAGE) ? BM
+                   : ((BM / 2) * LDC * 4 <= S * STAGE) ? BM / 2
+                   : ((BM / 4) * LDC * 4 <= S * STAGE) ? BM / 4 : BM / 8;
+  static_assert(HR % 16 == 0 && HR * LDC * 4 <= S * STAGE, "epilogue staging must fit in the LDS image");
   float* cs = (float*)smem;
   CT* Cb = (CT*)p.C + (long long)batch * p.c_bs + (p.c_mode == 3 ? (long long)split * p.slab : 0);
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
   constexpr int GPR = BN / 8;            // 8-column groups per row
   constexpr int RPP = NT / GPR;          // rows per pass
 #pragma unroll 1
-  for (int half = 0; half < 2; ++half) {
-    if (wm == half) {
+  for (int pass = 0; pass < BM / HR; ++pass) {
+    {
       const int g = lane >> 4;
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+      for (int i = 0; i < RM; ++i) {
+        const int rb = wm * TM + i * 16 - pass * HR;  // block's first row within this pass
+        if (rb < 0 || rb >= HR) continue;
 #pragma unroll
         for (int j = 0; j < RN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            cs[(i * 16 + 4 * g + r) * LDC + wn * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r] * p.alpha;
+            cs[(rb + 4 * g + r) * LDC + wn * TN + j * 16 + (lane & 15)] = acc[i][j][r] * p.alpha;
+      }
     }
     __syncthreads();
 #pragma unroll 1
     for (int rr = tid / GPR; rr < HR; rr += RPP) {
-      const int row = m0 + half * HR + rr;
+      const int row = m0 + pass * HR + rr;
       if (row >= p.M) continue;
       long long drow = row;
       if (p.row_map == 1) {  // stride-2 dgrad scatter: row over (n, oy, ox) -> (n, 2oy, 2ox)
@@ -468,22 +515,83 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Dispatch: choose tile by N, grid = (ceil(M/BM), ceil(N/BN), batch * nsplit)
+// Tile configurations and dispatch.  grid = (ceil(M/BM), ceil(N/BN), batch * nsplit)
 // ---------------------------------------------------------------------------------------
-template <class T, class CT, int BM, int BN, int LA, int LB>
-static int launch_t(const GemmArgs& a, int batch, hipStream_t st) {
-  dim3 grid((a.M + BM - 1) / BM, (a.N + BN - 1) / BN, batch * a.nsplit);
-  hipLaunchKernelGGL((gemm_kernel<T, CT, BM, BN, LA, LB>), grid, dim3(NT), 0, st, a);
+struct TileCfg { int bm, bn, wm, wn, s; };
+// bf16 configurations (index = config id); fp32 (parity path) always uses id 1's tile with S=2
+static constexpr TileCfg kCfg[] = {
+    {128, 64, 2, 2, 2},   // 0: small grids
+    {128, 128, 2, 2, 2},  // 1
+    {128, 128, 2, 2, 3},  // 2
+    {256, 128, 4, 2, 3},  // 3
+    {128, 256, 2, 4, 3},  // 4
+    {256, 256, 2, 4, 2},  // 5
+    {128, 64, 2, 2, 4},   // 6
+    {128, 128, 2, 2, 4},  // 7
+    {256, 128, 4, 2, 2},  // 8
+    {128, 256, 2, 4, 2},  // 9
+    {256, 256, 4, 2, 2},  // 10
+    {128, 128, 4, 2, 2},  // 11: 8 waves of 32x64
+    {128, 64, 4, 2, 2},   // 12: 8 waves of 32x32
+};
+constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
+static int g_force_cfg = -1;
+
+static long long cfg_blocks(int c, const GemmArgs& a, int batch) {
+  return (long long)((a.M + kCfg[c].bm - 1) / kCfg[c].bm) * ((a.N + kCfg[c].bn - 1) / kCfg[c].bn) *
+         batch * a.nsplit;
+}
+
+// Shape heuristic (tools/gemm_cfg_sweep.py on the step's conv shapes): 8-wave tiles win
+// everywhere except N <= 64; 256x256 once it still gives ~200+ blocks, 128x256 for N >= 256
+// at ~200+ blocks, 128x128 (8 waves of 32x64) otherwise.
+static int heuristic_cfg(int M, int N, int bz) {
+  GemmArgs a = {};
+  a.M = M; a.N = N; a.nsplit = 1;
+  if (N <= 64) return 12;
+  if (N >= 512 && cfg_blocks(10, a, bz) >= 200) return 10;
+  if (N >= 256 && cfg_blocks(9, a, bz) >= 200) return 9;
+  return 11;
+}
+
+static int pick_cfg(const GemmArgs& a, int batch) {
+  if (g_force_cfg >= 0 && g_force_cfg < kNumCfg) return g_force_cfg;
+  if (a.cfg >= 0 && a.cfg < kNumCfg) return a.cfg;
+  return heuristic_cfg(a.M, a.N, batch * a.nsplit);
+}
+
+template <class T, class CT, int C, int LA, int LB>
+static int launch_c(const GemmArgs& a, int batch, hipStream_t st) {
+  constexpr TileCfg c = kCfg[C];
+  dim3 grid((a.M + c.bm - 1) / c.bm, (a.N + c.bn - 1) / c.bn, batch * a.nsplit);
+  hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB>), grid,
+                     dim3(c.wm * c.wn * 64), 0, st, a);
   CN_CHECK_LAUNCH();
   return 0;
 }
 
 template <class T, class CT, int LA, int LB>
 static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
-  // 128x128 when it yields >= 1.5 waves of blocks over the 256 CUs, else 128x64
-  long long t128 = (long long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch * a.nsplit;
-  if (a.N <= 64 || t128 < 384) return launch_t<T, CT, 128, 64, LA, LB>(a, batch, st);
-  return launch_t<T, CT, 128, 128, LA, LB>(a, batch, st);
+  if constexpr (sizeof(T) == 4) {
+    if (a.N <= 64 || cfg_blocks(1, a, batch) < 384) return launch_c<T, CT, 0, LA, LB>(a, batch, st);
+    return launch_c<T, CT, 1, LA, LB>(a, batch, st);
+  } else {
+    switch (pick_cfg(a, batch)) {
+      case 0: return launch_c<T, CT, 0, LA, LB>(a, batch, st);
+      case 1: return launch_c<T, CT, 1, LA, LB>(a, batch, st);
+      case 2: return launch_c<T, CT, 2, LA, LB>(a, batch, st);
+      case 3: return launch_c<T, CT, 3, LA, LB>(a, batch, st);
+      case 4: return launch_c<T, CT, 4, LA, LB>(a, batch, st);
+      case 5: return launch_c<T, CT, 5, LA, LB>(a, batch, st);
+      case 6: return launch_c<T, CT, 6, LA, LB>(a, batch, st);
+      case 7: return launch_c<T, CT, 7, LA, LB>(a, batch, st);
+      case 8: return launch_c<T, CT, 8, LA, LB>(a, batch, st);
+      case 9: return launch_c<T, CT, 9, LA, LB>(a, batch, st);
+      case 10: return launch_c<T, CT, 10, LA, LB>(a, batch, st);
+      case 11: return launch_c<T, CT, 11, LA, LB>(a, batch, st);
+      default: return launch_c<T, CT, 12, LA, LB>(a, batch, st);
+    }
+  }
 }
 
 template <class T, class CT>
@@ -508,6 +616,24 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     return launch_kinds<float, float>(a, la, lb, batch, st);
   }
   return -11;
+}
+
+int cn_gemm_pick(int M, int N, int batch_splits) {
+  if (g_force_cfg >= 0 && g_force_cfg < kNumCfg) return g_force_cfg;
+  return heuristic_cfg(M, N, batch_splits);
+}
+
+long long cn_gemm_cfg_blocks(int cfg, int M, int N) {
+  GemmArgs a = {};
+  a.M = M; a.N = N; a.nsplit = 1;
+  return cfg_blocks(cfg, a, 1);
+}
+
+// Development hook: force one tile configuration for every bf16 launch (-1 = heuristic).
+extern "C" int cn_gemm_force_config(int cfg) {
+  if (cfg >= kNumCfg) return -1;
+  g_force_cfg = cfg;
+  return kNumCfg;
 }
 
 // Split-K reduction: out[i] (+)= sum_s ws[s * slab + i]  (fp32, float4-vectorised, fixed order

@@ -158,6 +158,9 @@ int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
               float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C, void* y,
               long long ldy, int accumulate, hipStream_t stream);
+/* Development hook (tuning tools only): force GEMM tile configuration `cfg` for every bf16
+ * launch; -1 restores the shape heuristic.  Returns the number of configurations. */
+int cn_gemm_force_config(int cfg);
 
 #ifdef __cplusplus
 }
