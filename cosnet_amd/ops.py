@@ -57,10 +57,15 @@ class GemmProfile:
         t = sum(r[1].elapsed_time(r[2]) for r in self.rec) * 1e-3
         return len(self.rec), fl, t
 
+    def algorithmic_bytes(self):
+        """Total unique operand bytes of the recorded launches: each GEMM's inputs read once
+        (the conv input tensor itself, not its implicit im2col) plus its output written once."""
+        return sum(r[4] for r in self.rec)
+
     def by_tag(self):
         """{tag: [launches, FLOPs, seconds]} -- tag = (op, M, N, K) of each launch."""
         out = {}
-        for fl, e0, e1, tag in self.rec:
+        for fl, e0, e1, tag, _ in self.rec:
             r = out.setdefault(tag, [0, 0.0, 0.0])
             r[0] += 1
             r[1] += fl
@@ -68,7 +73,7 @@ class GemmProfile:
         return out
 
 
-def _prof_start(flops, tag=None):
+def _prof_start(flops, tag=None, nbytes=0):
     p = GemmProfile.active
     if p is None:
         return None
@@ -77,7 +82,7 @@ def _prof_start(flops, tag=None):
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    p.rec.append((flops, e0, e1, tag))
+    p.rec.append((flops, e0, e1, tag, nbytes))
     return e1
 
 
@@ -127,7 +132,9 @@ def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
     oh, ow = out_hw(h, w, k, stride, pad, dil)
     if out is None:
         out = torch.empty((n * oh * ow, cout), dtype=x.dtype, device=x.device)
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("fwd", n * oh * ow, cout, k * k * cin))
+    es = x.element_size()
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("fwd", n * oh * ow, cout, k * k * cin),
+                     es * (n * h * w * cin + cout * k * k * cin + n * oh * ow * cout))
     nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
             stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
     _prof_end(ev)
@@ -138,7 +145,9 @@ def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accu
     cout = wt.shape[1] // (k * k)
     if out is None:
         out = torch.empty((n * h * w, cin), dtype=dy.dtype, device=dy.device)
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("dgrad%d" % stride, n * h * w, cin, k * k * cout))
+    es = dy.element_size()
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("dgrad%d" % stride, n * h * w, cin, k * k * cout),
+                     es * (n * oh * ow * cout + cout * k * k * cin + n * h * w * cin))
     nv.call("cn_conv_dgrad", dtc(dy), dy.data_ptr(), ld(dy), n, oh, ow, cout, wt.data_ptr(), cin,
             k, k, stride, pad, dil, out.data_ptr(), ld(out), h, w, int(accumulate), nv.stream())
     _prof_end(ev)
@@ -151,7 +160,9 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
         dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
     nws = int(nv.query("cn_conv_wgrad_workspace_floats", dtc(x), n, oh, ow, cout, k, k, cin))
     ws = torch.empty((nws,), dtype=torch.float32, device=x.device) if nws else None
-    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("wgrad", cout, k * k * cin, n * oh * ow))
+    es = x.element_size()
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("wgrad", cout, k * k * cin, n * oh * ow),
+                     es * (n * h * w * cin + n * oh * ow * cout) + 4 * cout * k * k * cin)
     nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
             ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.ptr(ws), nv.stream())
     _prof_end(ev)
@@ -208,7 +219,10 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
         c_bs = m * n
     c_f32 = int(out.dtype == torch.float32)
     ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k),
-                     ("gemm%d%d" % (layout_a, layout_b), batch * m, n, k))
+                     ("gemm%d%d" % (layout_a, layout_b), batch * m, n, k),
+                     (batch if a_bs else 1) * m * k * a.element_size() +
+                     (batch if b_bs else 1) * n * k * b.element_size() +
+                     batch * m * n * out.element_size())
     if nsplit > 1 and c_mode in (0, 1) and batch == 1 and c_f32 and ldc == n:
         # split-K into fp32 slabs + fixed-order reduction (no atomic contention)
         slab = m * n

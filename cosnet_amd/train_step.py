@@ -29,6 +29,8 @@ from .ops import WeightCache
 
 
 class TrainStep:
+    """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
+
     def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None):
         self.model, self.opt = model, opt
         self.l1 = float(l1_weight)
@@ -36,15 +38,17 @@ class TrainStep:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         dev = next(model.parameters()).device
-        b, s = batch, size
-        self.rgb_a = torch.zeros((b, 3, s, s), device=dev)
+        b = batch
+        h, w = (size, size) if isinstance(size, int) else tuple(size)
+        self.hw = (h, w)
+        self.rgb_a = torch.zeros((b, 3, h, w), device=dev)
         self.rgb_b = torch.zeros_like(self.rgb_a)
-        self.dep_a = torch.zeros((b, 1, s, s), device=dev)
+        self.dep_a = torch.zeros((b, 1, h, w), device=dev)
         self.dep_b = torch.zeros_like(self.dep_a)
-        self.gt_a = torch.zeros((b, 1, s, s), device=dev)
+        self.gt_a = torch.zeros((b, 1, h, w), device=dev)
         self.gt_b = torch.zeros_like(self.gt_a)
         self.cnt = torch.zeros((2,), dtype=torch.int64, device=dev)
-        self.total = b * s * s * self.world
+        self.total = b * h * w * self.world
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
         self.params = []
         seen = set()

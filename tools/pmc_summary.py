@@ -67,8 +67,11 @@ def main():
              "write_bytes_per_launch": f["write_bytes"] / n,
              "traffic_bytes_per_launch": (f["read_bytes"] + f["write_bytes"]) / n,
              "traffic_bytes_total": f["read_bytes"] + f["write_bytes"]}
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in f and f.get("SQ_BUSY_CU_CYCLES"):
-            e["mfma_busy_frac_of_cu_busy"] = f["SQ_VALU_MFMA_BUSY_CYCLES"] / f["SQ_BUSY_CU_CYCLES"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in f and f.get("GRBM_GUI_ACTIVE"):
+            # MFMA_BUSY = matrix-pipe cycles summed over every SIMD (32 per 32x32x16 bf16 MFMA);
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs -> /8 = elapsed GPU cycles.
+            # utilisation = busy / (1024 SIMDs * elapsed cycles)
+            e["mfma_util"] = f["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * f["GRBM_GUI_ACTIVE"] / 8.0)
         for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES", "GRBM_GUI_ACTIVE"):
             if c in f:
                 e[c] = f[c]
