@@ -518,7 +518,11 @@ __global__ void sum_partials_k(const float* __restrict__ partial, int n, float s
 }
 
 // ---- SGD (torch.optim.SGD semantics: d = g + wd*p; buf = mom*buf + d (buf = d first);
-//      p -= lr * buf), multi-tensor; then refresh the compute-dtype copy ----------------------
+//      p -= lr * buf), multi-tensor, fused with the refresh of the compute-dtype weight copies
+//      the GEMMs read (wf [Cout][KHW][Cp], wt [Cin][KHW][Cout]) -------------------------------
+// One record = one work item of one parameter: a flat element range (mode 0) or a range of
+// 64x64 (co, ci) tiles of one tap (mode 1: coalesced fp32 reads/writes along ci, the new
+// weights staged through LDS so the transposed copy is written coalesced along co).
 struct SgdTensor {
   float* p;
   const float* g;
@@ -526,20 +530,130 @@ struct SgdTensor {
   long long n;
   int group;
   int first;
+  void* wf;
+  void* wt;
+  int cout, khw, cin, cp;
+  int wdt;   // 0: no copy, 1: bf16 copies, 2: fp32 copies
+  int mode;  // 0: elements [beg, end); 1: tiles [beg, end)
+  long long beg, end;
 };
+static_assert(sizeof(SgdTensor) == 96, "SgdTensor layout is shared with cosnet_amd/optim.py");
 
-__global__ void sgd_k(const SgdTensor* __restrict__ ts, int nt, const float* __restrict__ lrs,
-                      float wd, float mom) {
-  for (int t = blockIdx.y; t < nt; t += gridDim.y) {
-    SgdTensor T = ts[t];
+__device__ __forceinline__ float sgd_upd(float& p, float g, float& b, float lr, float wd, float mom,
+                                         int first) {
+  float d = g + wd * p;
+  b = first ? d : fmaf(mom, b, d);
+  p -= lr * b;
+  return p;
+}
+
+__device__ __forceinline__ void put_w(void* base, long long idx, float v, int wdt) {
+  if (wdt == 1) ((bf16*)base)[idx] = (bf16)v;
+  else ((float*)base)[idx] = v;
+}
+
+__global__ __launch_bounds__(256) void sgd_k(const SgdTensor* __restrict__ ts, int nt,
+                                             const float* __restrict__ lrs, float wd, float mom) {
+  __shared__ float tile[64][65];
+  const int tid = threadIdx.x;
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    const SgdTensor T = ts[t];
     if (!T.g) continue;
-    float lr = lrs[T.group];
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < T.n;
-         i += (long long)gridDim.x * blockDim.x) {
-      float d = T.g[i] + wd * T.p[i];
-      float b = T.first ? d : fmaf(mom, T.buf[i], d);
-      T.buf[i] = b;
-      T.p[i] -= lr * b;
+    const float lr = lrs[T.group];
+    if (T.mode == 0) {
+      if (T.wdt == 0 && (T.beg & 3) == 0 && ((T.end - T.beg) & 3) == 0 &&
+          ((uintptr_t)T.p & 15) == 0 && ((uintptr_t)T.g & 15) == 0 && ((uintptr_t)T.buf & 15) == 0) {
+        for (long long i = T.beg + 4 * tid; i < T.end; i += 4 * 256) {
+          f32x4 p = *(const f32x4*)(T.p + i), g = *(const f32x4*)(T.g + i);
+          f32x4 b = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + i);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float pe = p[e], be = b[e];
+            sgd_upd(pe, g[e], be, lr, wd, mom, T.first);
+            p[e] = pe;
+            b[e] = be;
+          }
+          *(f32x4*)(T.p + i) = p;
+          *(f32x4*)(T.buf + i) = b;
+        }
+      } else {
+        for (long long i = T.beg + tid; i < T.end; i += 256) {
+          float p = T.p[i], b = T.first ? 0.f : T.buf[i];
+          float v = sgd_upd(p, T.g[i], b, lr, wd, mom, T.first);
+          T.p[i] = p;
+          T.buf[i] = b;
+          if (T.wdt) {
+            int ci = (int)(i % T.cin);
+            long long r = i / T.cin;
+            int tap = (int)(r % T.khw), co = (int)(r / T.khw);
+            put_w(T.wf, ((long long)co * T.khw + tap) * T.cp + ci, v, T.wdt);
+            if (T.wt) put_w(T.wt, ((long long)ci * T.khw + tap) * T.cout + co, v, T.wdt);
+          }
+        }
+      }
+      continue;
+    }
+    // mode 1: cin % 4 == 0
+    const int ncob = (T.cout + 63) >> 6, ncib = (T.cin + 63) >> 6;
+    for (long long tl = T.beg; tl < T.end; ++tl) {
+      const int cib = (int)(tl % ncib);
+      const long long r0 = tl / ncib;
+      const int cob = (int)(r0 % ncob), tap = (int)(r0 / ncob);
+      const int co0 = cob * 64, ci0 = cib * 64;
+      const int rr = tid >> 4, c4 = (tid & 15) * 4;
+      const int ci = ci0 + c4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = co0 + rr + 16 * j;
+        if (co < T.cout && ci < T.cin) {
+          const long long idx = ((long long)co * T.khw + tap) * T.cin + ci;
+          f32x4 p = *(const f32x4*)(T.p + idx), g = *(const f32x4*)(T.g + idx);
+          f32x4 b = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + idx);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float pe = p[e], be = b[e];
+            sgd_upd(pe, g[e], be, lr, wd, mom, T.first);
+            p[e] = pe;
+            b[e] = be;
+          }
+          *(f32x4*)(T.p + idx) = p;
+          *(f32x4*)(T.buf + idx) = b;
+          const long long fo = ((long long)co * T.khw + tap) * T.cp + ci;
+          if (T.wdt == 1) {
+            bf16* w = (bf16*)T.wf + fo;
+            w[0] = (bf16)p[0]; w[1] = (bf16)p[1]; w[2] = (bf16)p[2]; w[3] = (bf16)p[3];
+          } else {
+            float* w = (float*)T.wf + fo;
+            w[0] = p[0]; w[1] = p[1]; w[2] = p[2]; w[3] = p[3];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tile[rr + 16 * j][c4 + e] = p[e];
+        }
+      }
+      if (T.wt) {
+        __syncthreads();
+        // wt rows ci (64 per tile), 16 consecutive co per thread
+        const int cil = tid >> 2, seg = (tid & 3) * 16;
+        const int cw = ci0 + cil;
+        if (cw < T.cin) {
+          const long long ro = ((long long)cw * T.khw + tap) * T.cout;
+          if (T.wdt == 1 && (T.cout & 7) == 0 && co0 + seg + 16 <= T.cout) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = tile[seg + e][cil];
+            u32x4* dst = (u32x4*)((bf16*)T.wt + ro + co0 + seg);
+            dst[0] = Chunk<bf16>::pack(v);
+            dst[1] = Chunk<bf16>::pack(v + 8);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int co = co0 + seg + e;
+              if (co < T.cout) put_w(T.wt, ro + co, tile[seg + e][cil], T.wdt);
+            }
+          }
+        }
+        __syncthreads();
+      }
     }
   }
 }
@@ -841,7 +955,8 @@ extern "C" int cn_bce_l1_devcount(const float* pred, const float* gt, long long 
 
 extern "C" int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float momentum,
                       hipStream_t st) {
-  dim3 grid(64, nt < 1024 ? nt : 1024);
+  if (nt <= 0) return 0;
+  dim3 grid(nt < 8192 ? nt : 8192);
   hipLaunchKernelGGL(sgd_k, grid, dim3(256), 0, st, (const SgdTensor*)tensors, nt, lrs, wd, momentum);
   CN_CHECK_LAUNCH();
   return 0;

@@ -16,9 +16,12 @@ import numpy as np
 import torch
 
 from . import _native as nv
-from .ops import WeightCache
+from .ops import WCACHE, WeightCache
 
-_REC = struct.Struct("<QQQqii")  # SgdTensor: p, g, buf, n, group, first
+# SgdTensor (ew.hip): p, g, buf, n, group, first, wf, wt, cout, khw, cin, cp, wdt, mode, beg, end
+_REC = struct.Struct("<QQQqiiQQiiiiiiqq")
+_FLAT_CHUNK = 1 << 16      # elements per flat work item
+_TILE_CHUNK = 16           # 64x64 tiles per tiled work item
 
 
 def reference_param_groups(model, duplicate_params=False):
@@ -63,7 +66,7 @@ class SGD:
     def reserve(self, counts=None):
         """Allocate the pinned / device staging of the SGD tables (records per launch)."""
         if counts is None:
-            counts = [sum(len(g) for g in self.groups)]
+            counts = self._max_counts()
         dev = self.groups[0][0].device if self.groups[0] else self.groups[1][0].device
         self._stage, self._stage_cap = [], []
         for n in counts:
@@ -73,6 +76,25 @@ class SGD:
         self._table_key = None
         if self._lr_dev is None:
             self._lr_dev = torch.zeros((len(self.lrs),), dtype=torch.float32, device=dev)
+
+    def _max_counts(self):
+        """Upper bound of the work items per launch (step() splits launches at duplicates)."""
+        counts, cur, seen = [], 0, set()
+        for g in self.groups:
+            for p in g:
+                if id(p) in seen:
+                    counts.append(cur)
+                    cur, seen = 0, set()
+                seen.add(id(p))
+                n = p.numel()
+                flat = -(-n // _FLAT_CHUNK)
+                tiles = 0
+                if p.dim() >= 2:
+                    khw = p.shape[2] * p.shape[3] if p.dim() == 4 else 1
+                    tiles = -(-(khw * (-(-p.shape[0] // 64)) * (-(-p.shape[1] // 64))) // _TILE_CHUNK)
+                cur += max(1, flat, tiles)
+        counts.append(cur)
+        return counts
 
     def zero_grad(self, set_to_none=True):
         for g in self.groups:
@@ -87,7 +109,10 @@ class SGD:
         self.lrs = list(lrs)
 
     def _records(self):
-        recs, keep = [], []
+        """Work items of this step: (param record..., chunking) tuples for cn_sgd, plus the
+        weight-cache entries the kernel refreshes."""
+        recs, keep, refreshed = [], [], []
+        start = {}
         for gi, g in enumerate(self.groups):
             for p in g:
                 if p.grad is None:
@@ -95,21 +120,42 @@ class SGD:
                 if p.grad.dtype != torch.float32 or not _dense(p.grad, p):
                     p.grad = p.grad.contiguous(memory_format=_fmt(p))
                 st = self.state.get(id(p))
-                first = 0
                 if st is None:
                     st = {"momentum_buffer": torch.empty_like(p), "steps": 0}
                     self.state[id(p)] = st
-                if st["steps"] == 0:
-                    first = 1
+                # torch's for-loop SGD gathers every entry's momentum buffer BEFORE updating:
+                # on a parameter's first step, each duplicate entry starts its own buffer
+                # (buf = d), later steps share the one buffer
+                if id(p) not in start:
+                    start[id(p)] = st["steps"]
+                first = int(start[id(p)] == 0)
                 st["steps"] += 1
                 buf = st["momentum_buffer"]
-                recs.append((p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), p.numel(), gi, first))
+                ents = WCACHE.entries(p)
+                copy = (0, 0, 0, 0, 0, 0, 0)
+                if ents:
+                    wf, wt, cout, khw, cin, cp, ent = ents[0]
+                    wdt = 1 if wf.dtype == torch.bfloat16 else 2
+                    copy = (wf.data_ptr(), wt.data_ptr() if wt is not None else 0, cout, khw, cin, cp, wdt)
+                    refreshed.append(ent)
+                    for e in ents[1:]:
+                        WeightCache.invalidate(e[6])
+                head = (p.data_ptr(), p.grad.data_ptr(), buf.data_ptr(), p.numel(), gi, first) + copy
+                n = p.numel()
+                cout, khw, cin = copy[2], copy[3], copy[4]
+                if copy[6] and cin % 4 == 0 and n == cout * khw * cin:
+                    ntiles = khw * (-(-cout // 64)) * (-(-cin // 64))
+                    for b in range(0, ntiles, _TILE_CHUNK):
+                        recs.append(head + (1, b, min(ntiles, b + _TILE_CHUNK)))
+                else:
+                    for b in range(0, n, _FLAT_CHUNK):
+                        recs.append(head + (0, b, min(n, b + _FLAT_CHUNK)))
                 keep.append(p)
-        return recs, keep
+        return recs, keep, refreshed
 
     @torch.no_grad()
     def step(self):
-        recs, _ = self._records()
+        recs, _, refreshed = self._records()
         if not recs:
             return
         dev = self.groups[0][0].device if self.groups[0] else self.groups[1][0].device
@@ -117,11 +163,11 @@ class SGD:
         # order (torch's for-loop SGD over duplicated param-group entries)
         batches, cur, seen = [], [], set()
         for r in recs:
-            if r[0] in seen:
+            if (r[0], r[-2]) in seen:  # same parameter AND same work item: a duplicate entry
                 batches.append(cur)
                 cur, seen = [], set()
             cur.append(r)
-            seen.add(r[0])
+            seen.add((r[0], r[-2]))
         batches.append(cur)
         self._upload_lrs(dev)
         key = tuple(tuple(b) for b in batches)
@@ -154,7 +200,10 @@ class SGD:
         for host, devt, nrec in self._tables:
             nv.call("cn_sgd", devt.data_ptr(), nrec, self._lr_dev.data_ptr(), self.weight_decay,
                     self.momentum, nv.stream())
-        WeightCache.epoch += 1
+        # the kernel rewrote the compute-dtype copies of every updated parameter that has
+        # one: those cache entries stay valid (no re-preparation before the next forward)
+        for ent in refreshed:
+            WCACHE.refreshed(ent)
 
     def _upload_lrs(self, dev):
         if self._lr_dev is None:

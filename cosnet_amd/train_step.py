@@ -25,7 +25,6 @@ import torch
 import torch.distributed as dist
 
 from . import functions as fn
-from .ops import WeightCache
 
 
 class TrainStep:
@@ -177,7 +176,8 @@ class TrainStep:
         self.opt.refresh_lrs()
         self._counts()
         self.graph.replay()
-        WeightCache.epoch += 1  # the replay updated the weights in place
+        # the replay updated the fp32 masters AND their compute-dtype copies in place (cn_sgd):
+        # the weight cache stays valid
         for m, d in self._nbt_delta.items():
             m._cn_nbt = getattr(m, "_cn_nbt", 0) + d
         if self.world > 1:

@@ -409,6 +409,58 @@ def test_sgd_step(cuda):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dup", [False, True])
+def test_sgd_refreshes_weight_copies(cuda, dt, dup):
+    """cn_sgd updates the fp32 masters AND rewrites the compute-dtype GEMM copies (forward
+    [Cout][KHW][Cp] and transposed [Cin][KHW][Cout]) in the same pass; the copies must equal a
+    fresh preparation from the updated masters, and the masters torch.optim.SGD's for-loop
+    semantics (duplicate entries updated once per occurrence)."""
+    from cosnet_amd.optim import SGD
+    g = torch.Generator().manual_seed(35)
+    shapes = [((96, 64, 3, 3), None), ((70, 36, 1, 1), None), ((64, 3, 7, 7), 8),
+              ((128, 256, 3, 3), None), ((256, 256), None), ((48,), None)]
+    ps = [torch.randn(s, generator=g) * 0.05 for s, _ in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = []
+    for p in ps:
+        q = p.clone().to(cuda)
+        if q.dim() == 4:
+            q = q.contiguous(memory_format=torch.channels_last)
+        mine.append(torch.nn.Parameter(q))
+    for (s, cp), q in zip(shapes, mine):  # cache entries exist before the first step
+        if q.dim() >= 2:
+            ops.WCACHE.get(q, dt, cin_pad=cp, need_t=cp is None)
+    g0 = mine[:2] + (mine[:1] if dup else [])
+    r0 = ref[:2] + (ref[:1] if dup else [])
+    opt = torch.optim.SGD([{"params": r0, "lr": 0.01}, {"params": ref[2:], "lr": 0.1}],
+                          lr=0.01, momentum=0.9, weight_decay=5e-4, foreach=False)
+    mopt = SGD([g0, mine[2:]], [0.01, 0.1])
+    for step in range(3):
+        for p in ref:
+            p.grad = torch.randn(p.shape, generator=g)
+        for p, r in zip(mine, ref):
+            p.grad = r.grad.clone().to(cuda)
+            if p.dim() == 4:
+                p.grad = p.grad.contiguous(memory_format=torch.channels_last)
+        opt.step()
+        mopt.step()
+    torch.cuda.synchronize()
+    for (s, cp), a, b in zip(shapes, mine, ref):
+        assert torch.allclose(a.detach().cpu(), b.detach(), atol=1e-6, rtol=1e-5), s
+        if a.dim() < 2:
+            continue
+        ents = ops.WCACHE.entries(a)
+        assert len(ents) == 1 and ents[0][6][0] is not None, "entry must stay valid after the step"
+        wf, wt = ents[0][0].clone(), ents[0][1]
+        wt = wt.clone() if wt is not None else None
+        ops.WeightCache.invalidate(ents[0][6])
+        rf, rt = ops.WCACHE.get(a, dt, cin_pad=cp, need_t=cp is None)
+        assert torch.equal(wf, rf), s
+        if wt is not None:
+            assert torch.equal(wt, rt), s
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("hw", [(13, 13), (15, 20), (31, 41)])
 @pytest.mark.parametrize("both", [True, False])
 def test_coattention_block(cuda, dt, hw, both):
