@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (loads the HIP runtime the library binds to)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libcosnet_hip.so")
+# COSNET_HIP_LIB: development override (tools/ A/B builds); the package loads the in-tree build
+LIB_PATH = os.environ.get("COSNET_HIP_LIB") or os.path.join(_HERE, "_lib", "libcosnet_hip.so")
 
 DT_F32 = 0
 DT_BF16 = 1

@@ -304,6 +304,13 @@ __device__ __forceinline__ void raw_barrier() {
 // tile kt is consumed, and each K step ends with a COUNTED wait for tile kt+1 only (the
 // younger S-2 tiles stay in flight across the barrier) -- one barrier per K step.
 // ---------------------------------------------------------------------------------------
+#ifndef CN_GEMM_GROUP_M
+#define CN_GEMM_GROUP_M 8
+#endif
+#ifndef CN_GEMM_PRIO
+#define CN_GEMM_PRIO 0
+#endif
+
 template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
@@ -335,8 +342,22 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
       const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
       lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
     }
+#if CN_GEMM_GROUP_M > 0
+    // grouped order: each run of GROUP_M M-tiles walks all its N-tiles before the next run,
+    // so the blocks resident on one XCD share A panels (and the B panel) in its L2
+    {
+      const int gm = CN_GEMM_GROUP_M;
+      const int per = gm * gridDim.y;
+      const int grp = lin / per, first = grp * gm;
+      const int gsz = min((int)gridDim.x - first, gm);
+      const int r = lin - grp * per;
+      tm = first + r % gsz;
+      tn = r / gsz;
+    }
+#else
     tm = lin % gridDim.x;
     tn = lin / gridDim.x;
+#endif
   }
   const int m0 = tm * BM, n0 = tn * BN;
   const int bz = blockIdx.z;
@@ -370,6 +391,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
   wait_tiles<G>(min(nt - 1, S - 2));
   raw_barrier();
 
+#if CN_GEMM_PRIO == 2
+  if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   int cur = 0;                     // stage of tile kt
   int nxt = S - 1;                 // stage of tile kt + S - 1
   for (int kt = 0; kt < nt; ++kt) {
@@ -388,11 +412,17 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
         for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, AMC>(As, wm * TM + i * 16, pc, lane);
 #pragma unroll
         for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, BMC>(Bs, wn * TN + j * 16, pc, lane);
+#if CN_GEMM_PRIO == 1
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int i = 0; i < RM; ++i)
 #pragma unroll
           for (int j = 0; j < RN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#if CN_GEMM_PRIO == 1
+        __builtin_amdgcn_s_setprio(0);
+#endif
       } else {
         f32x4 af[RM], bfr[RN];
         if (!AMC) {

@@ -1,0 +1,66 @@
+"""Time ONE implicit-GEMM shape in isolation (for PMC passes over a single kernel).
+
+    python tools/gemm_probe.py SHAPE [cfg] [reps]
+SHAPE: aspp_fwd | aspp_wgrad | l3_fwd | l3_dgrad | l3_wgrad | l3_1x1 | dense8k
+"""
+import sys
+
+import torch
+
+sys.path.insert(0, '.')
+from cosnet_amd import _native as nv  # noqa: E402
+from cosnet_amd import ops  # noqa: E402
+
+dev = torch.device('cuda:0')
+dt = torch.bfloat16
+CONV = {  # n, cin, h, w, cout, k, stride, pad, dil
+    "aspp": (8, 2048, 60, 60, 512, 3, 1, 12, 12),
+    "l3": (8, 256, 60, 60, 256, 3, 1, 2, 2),
+    "l3_1x1": (8, 1024, 60, 60, 256, 1, 1, 0, 1),
+}
+
+
+def main():
+    name = sys.argv[1]
+    cfg = int(sys.argv[2]) if len(sys.argv) > 2 else -1
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
+    nv.load().cn_gemm_force_config(cfg)
+    if name == "dense8k":
+        m = n = k = 8192
+        a = torch.randn(m, k, device=dev).to(dt)
+        b = torch.randn(n, k, device=dev).to(dt)
+        c = torch.empty(m, n, device=dev, dtype=dt)
+        fl = 2.0 * m * n * k
+        fn = lambda: ops.gemm(a, b, m, n, k, lda=k, ldb=k, out=c, ldc=n)  # noqa: E731
+    else:
+        key, op = name.rsplit("_", 1) if name != "l3_1x1" else ("l3_1x1", "fwd")
+        n, cin, h, w, cout, kk, s, p, d = CONV[key]
+        x = torch.randn(n * h * w, cin, device=dev).to(dt)
+        wp = (torch.randn(cout, cin, kk, kk, device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
+        wf, wt = ops.WCACHE.get(wp, dt)
+        y, oh, ow = ops.conv_fwd(x, n, h, w, wf, cout, kk, s, p, d)
+        fl = 2.0 * n * oh * ow * cout * kk * kk * cin
+        dy = torch.randn_like(y)
+        dx = torch.empty_like(x)
+        dw = torch.zeros(cout, kk * kk * cin, device=dev)
+        if op == "fwd":
+            fn = lambda: ops.conv_fwd(x, n, h, w, wf, cout, kk, s, p, d, out=y)  # noqa: E731
+        elif op == "dgrad":
+            fn = lambda: ops.conv_dgrad(dy, n, oh, ow, wt, cin, kk, s, p, d, h, w, out=dx)  # noqa: E731
+        else:
+            fn = lambda: ops.conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, kk, s, p, d, dw=dw)  # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    print("%s cfg %d: %.1f us  %.0f TFLOP/s" % (name, cfg, t * 1e6, fl / t / 1e12), flush=True)
+
+
+if __name__ == "__main__":
+    main()
