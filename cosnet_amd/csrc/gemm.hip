@@ -40,8 +40,11 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 }
 
 // -------------------------------------------------------------------------------------
-// Operand loader.  ROWS = BM (A) or BN (B); NT threads.  Fills ROWS*8/NT 16-byte chunks per
-// thread per K tile (a tile is ROWS x 128 bytes of k).
+// Operand loader: LDS-DMA (global_load_lds_dwordx4) fill of one ROWS x 128-byte K tile per
+// call, NCH = ROWS*8/NT 16-byte chunks per thread.  Everything that does not change along K
+// (row / column pointers, the conv gather's per-chunk tap offsets, pixel coordinates) is
+// computed once in init(); issue() then costs a few VALU per chunk and advances the state by
+// one K tile (tiles are issued strictly in order, starting at kbeg).
 // -------------------------------------------------------------------------------------
 template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr int VEC = VecOf<T>::N;
@@ -52,176 +55,140 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr bool MC = (KIND == L_MC_DENSE || KIND == L_MC_CONV);
   static constexpr int CPR = ROWS / VEC;          // MC: chunks per k-row
   static constexpr int KROW_STEP = NT / CPR;      // MC: k-rows between a thread's chunks
+  static constexpr int RB = ROWS * (int)sizeof(T);  // MC: bytes per k-row of the LDS image
 
   const T* base;
   long long ld;
-  int lim;     // row / column bound (M or N)
-  int klim;    // k bound
-  // KC_CONV per-row state
+  int klim;             // k bound (zero beyond)
+  int kcol;             // KC: this thread's k offset within a tile (swizzled chunk * VEC)
+  const T* ptr[NCH];    // KC_DENSE: row pointer + kcol; MC_DENSE: next k-row pointer;
+                        // KC_CONV: pixel pointer of the cached tap (+ kcol)
+  bool ok[NCH];         // row / column / pixel validity
+  // KC_CONV
   int img[NCH], by[NCH], bx[NCH];
-  // MC_CONV per-thread column state
-  int ci, dy, dx;
-  bool colok;
+  int ctap;             // tap whose pixel pointers are cached (-1: none)
+  bool tap_uniform;     // C % BK == 0: a K tile never straddles two taps
+  // MC_CONV: per-chunk column (tap offsets, channel) and output-pixel coordinates
+  int ry[NCH], sx[NCH], cic[NCH];
+  int pim[NCH], poy[NCH], pox[NCH], pp[NCH];
+  int ax, ay, aim;      // advance of (ox, oy, im) per K tile
   ConvGeom g;
 
-  __device__ __forceinline__ void init(const T* b, long long ld_, int lim_, int klim_,
-                                       const ConvGeom& geo, int origin, int tid) {
-    base = b; ld = ld_; lim = lim_; klim = klim_;
-    if (KIND == L_KC_CONV) {
-      g = geo;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int row = origin + (tid >> 3) + RSTEP * i;
-        int rr = row < lim ? row : 0;
-        int q, rem, oy, ox;
-        fdivmod(rr, g.div_OHW, q, rem);
-        fdivmod(rem, g.div_OW, oy, ox);
-        img[i] = row < lim ? q : -1;
-        by[i] = oy * g.st + g.off_y;
-        bx[i] = ox * g.st + g.off_x;
-      }
-    }
-    if (KIND == L_MC_CONV) {
-      g = geo;
-      int n0 = origin + (tid % CPR) * VEC;
-      colok = n0 < lim;
-      int nn = colok ? n0 : 0;
-      int tap, r, s;
-      fdivmod(nn, g.div_C, tap, ci);
-      fdivmod(tap, g.div_KW, r, s);
-      dy = r * g.step_y + g.off_y;
-      dx = s * g.step_x + g.off_x;
-    }
-  }
-
-  __device__ __forceinline__ void load(int k0, int origin, int tid, u32x4* v) const {
-    const u32x4 zero = {0u, 0u, 0u, 0u};
-    if (KIND == L_KC_DENSE) {
-      int k = k0 + (tid & 7) * VEC;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int row = origin + (tid >> 3) + RSTEP * i;
-        bool ok = row < lim && k < klim;
-        v[i] = ok ? *(const u32x4*)(base + (long long)row * ld + k) : zero;
-      }
-    } else if (KIND == L_KC_CONV) {
-      int k = k0 + (tid & 7) * VEC;
-      int tap, c, r, s;
-      fdivmod(k < klim ? k : 0, g.div_C, tap, c);
-      fdivmod(tap, g.div_KW, r, s);
-      int oy = r * g.step_y, ox = s * g.step_x;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int y = by[i] + oy, x = bx[i] + ox;
-        bool ok = img[i] >= 0 && k < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-        long long pix = ((long long)img[i] * g.H + y) * g.W + x;
-        v[i] = ok ? *(const u32x4*)(base + pix * ld + c) : zero;
-      }
-    } else if (KIND == L_MC_DENSE) {
-      int col = origin + (tid % CPR) * VEC;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int kr = k0 + tid / CPR + KROW_STEP * i;
-        bool ok = kr < klim && col < lim;
-        v[i] = ok ? *(const u32x4*)(base + (long long)kr * ld + col) : zero;
-      }
-    } else {  // L_MC_CONV
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int p = k0 + tid / CPR + KROW_STEP * i;
-        int pp = p < klim ? p : 0;
-        int im, rem, oy, ox;
-        fdivmod(pp, g.div_OHW, im, rem);
-        fdivmod(rem, g.div_OW, oy, ox);
-        int y = oy * g.st + dy, x = ox * g.st + dx;
-        bool ok = colok && p < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-        long long pix = ((long long)im * g.H + y) * g.W + x;
-        v[i] = ok ? *(const u32x4*)(base + pix * ld + ci) : zero;
-      }
-    }
-  }
-
-  // LDS-DMA fill (global_load_lds_dwordx4): chunk q = tid + 256 i lands at byte 16 q of the
-  // tile (lane-linear per wave instruction); the XOR swizzle moves to the SOURCE chunk so the
-  // image is identical to store()'s.  Out-of-bounds chunks read the zero page.
-  __device__ __forceinline__ void issue(int k0, int origin, int tid, char* lds) const {
-    const void* zp = (const void*)g_zero16;
-    char* wbase = lds + (tid & ~63) * 16;
+  __device__ __forceinline__ void init(const T* b, long long ld_, int lim, int klim_,
+                                       const ConvGeom& geo, int origin, int tid, int kbeg) {
+    base = b; ld = ld_; klim = klim_;
     if (!MC) {
       const int pos = tid & 7;
-      const int c = pos ^ ((tid >> 3) & 7);  // row & 7 == (tid >> 3) & 7 for every i
-      const int k = k0 + c * VEC;
-      if (KIND == L_KC_DENSE) {
+      kcol = (pos ^ ((tid >> 3) & 7)) * VEC;  // row & 7 == (tid >> 3) & 7 for every chunk
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int row = origin + (tid >> 3) + RSTEP * i;
-          bool ok = row < lim && k < klim;
-          glds16(ok ? (const void*)(base + (long long)row * ld + k) : zp, wbase + i * NT * 16);
-        }
-      } else {  // L_KC_CONV
-        int tap, cc, r, ss;
-        fdivmod(k < klim ? k : 0, g.div_C, tap, cc);
-        fdivmod(tap, g.div_KW, r, ss);
-        int oy = r * g.step_y, ox = ss * g.step_x;
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          int y = by[i] + oy, x = bx[i] + ox;
-          bool ok = img[i] >= 0 && k < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-          long long pix = ((long long)img[i] * g.H + y) * g.W + x;
-          glds16(ok ? (const void*)(base + pix * ld + cc) : zp, wbase + i * NT * 16);
+      for (int i = 0; i < NCH; ++i) {
+        const int row = origin + (tid >> 3) + RSTEP * i;
+        ok[i] = row < lim;
+        const int rr = ok[i] ? row : 0;
+        if (KIND == L_KC_DENSE) {
+          ptr[i] = base + (long long)rr * ld + kcol;
+        } else {
+          int q, rem, oy, ox;
+          fdivmod(rr, geo.div_OHW, q, rem);
+          fdivmod(rem, geo.div_OW, oy, ox);
+          img[i] = ok[i] ? q : -1;
+          by[i] = oy * geo.st + geo.off_y;
+          bx[i] = ox * geo.st + geo.off_x;
         }
       }
+      if (KIND == L_KC_CONV) {
+        g = geo;
+        ctap = -1;
+        tap_uniform = (geo.C % BK) == 0;
+      }
     } else {
-      constexpr int RB = ROWS * (int)sizeof(T);
       const int pos = tid % CPR;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        const int krl = tid / CPR + KROW_STEP * i;          // k-row within the tile
+        const int krl = tid / CPR + KROW_STEP * i;  // k-row within the tile
         const int cchunk = (sizeof(T) == 2) ? (pos ^ (mc_swz(krl, RB / 8) >> 1)) : pos;
-        const int kr = k0 + krl;
         const int col = origin + cchunk * VEC;
-        const void* src = zp;
+        ok[i] = col < lim;
         if (KIND == L_MC_DENSE) {
-          if (kr < klim && col < lim) src = base + (long long)kr * ld + col;
-        } else {  // L_MC_CONV: n = (tap, ci) fixed per chunk column
-          int nn = col < lim ? col : 0;
-          int tap, cic, r, ss;
-          fdivmod(nn, g.div_C, tap, cic);
-          fdivmod(tap, g.div_KW, r, ss);
-          int pp = kr < klim ? kr : 0;
-          int im, rem, oy, ox;
-          fdivmod(pp, g.div_OHW, im, rem);
-          fdivmod(rem, g.div_OW, oy, ox);
-          int y = oy * g.st + r * g.step_y + g.off_y, x = ox * g.st + ss * g.step_x + g.off_x;
-          if (col < lim && kr < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W)
-            src = base + (((long long)im * g.H + y) * g.W + x) * ld + cic;
+          ptr[i] = base + (long long)(kbeg + krl) * ld + col;
+        } else {
+          const int nn = ok[i] ? col : 0;
+          int tap, r, s2;
+          fdivmod(nn, geo.div_C, tap, cic[i]);
+          fdivmod(tap, geo.div_KW, r, s2);
+          ry[i] = r * geo.step_y + geo.off_y;
+          sx[i] = s2 * geo.step_x + geo.off_x;
+          pp[i] = kbeg + krl;
+          int q, rem, oy, ox;
+          fdivmod(pp[i] < klim ? pp[i] : 0, geo.div_OHW, q, rem);
+          fdivmod(rem, geo.div_OW, oy, ox);
+          pim[i] = q; poy[i] = oy; pox[i] = ox;
         }
-        glds16(src, wbase + i * NT * 16);
+      }
+      if (KIND == L_MC_CONV) {
+        g = geo;
+        int q, rem, oy, ox;
+        fdivmod(BK, geo.div_OHW, q, rem);
+        fdivmod(rem, geo.div_OW, oy, ox);
+        aim = q; ay = oy; ax = ox;
       }
     }
   }
 
-  // LDS image: KC -> [ROWS][128 B] swizzled; MC -> [BK][ROWS*sizeof(T)] (bf16 swizzled)
-  __device__ __forceinline__ void store(char* lds, int tid, const u32x4* v) const {
-    if (!MC) {
+  // LDS-DMA fill: chunk q = tid + NT i lands at byte 16 q of the tile (lane-linear per wave
+  // instruction); the XOR swizzle lives in the SOURCE address so the image is the swizzled
+  // layout the fragment readers expect.  Out-of-bounds chunks read the zero page.
+  __device__ __forceinline__ void issue(int k0, char* lds, int tid) {
+    const void* zp = (const void*)g_zero16;
+    char* wbase = lds + (tid & ~63) * 16;
+    if (KIND == L_KC_DENSE) {
+      const bool kok = k0 + kcol < klim;
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int row = (tid >> 3) + RSTEP * i, c = tid & 7;
-        *(u32x4*)(lds + row * 128 + ((c ^ (row & 7)) << 4)) = v[i];
-      }
-    } else {
-      constexpr int RB = ROWS * (int)sizeof(T);  // bytes per k-row
+      for (int i = 0; i < NCH; ++i)
+        glds16((ok[i] && kok) ? (const void*)(ptr[i] + k0) : zp, wbase + i * NT * 16);
+    } else if (KIND == L_KC_CONV) {
+      const int k = k0 + kcol;
+      const bool kok = k < klim;
+      int tap, cc;
+      fdivmod(kok ? k : 0, g.div_C, tap, cc);
+      if (!tap_uniform || tap != ctap) {  // new tap: recompute the pixel pointers
+        int r, ss;
+        fdivmod(tap, g.div_KW, r, ss);
+        const int oy = r * g.step_y, ox = ss * g.step_x;
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        int kr = tid / CPR + KROW_STEP * i, cc = tid % CPR;
-        int off;
-        if (sizeof(T) == 2) {
-          int gr = (2 * cc) ^ mc_swz(kr, RB / 8);
-          off = kr * RB + gr * 8;
-        } else {
-          off = kr * RB + cc * 16;
+        for (int i = 0; i < NCH; ++i) {
+          const int y = by[i] + oy, x = bx[i] + ox;
+          const bool v = img[i] >= 0 && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+          ok[i] = v;
+          ptr[i] = base + (v ? (((long long)img[i] * g.H + y) * g.W + x) * ld : 0);
         }
-        *(u32x4*)(lds + off) = v[i];
+        ctap = tap;
+      }
+#pragma unroll
+      for (int i = 0; i < NCH; ++i)
+        glds16((ok[i] && kok) ? (const void*)(ptr[i] + cc) : zp, wbase + i * NT * 16);
+    } else if (KIND == L_MC_DENSE) {
+      const int kr0 = k0 + tid / CPR;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const bool v = ok[i] && kr0 + KROW_STEP * i < klim;
+        glds16(v ? (const void*)ptr[i] : zp, wbase + i * NT * 16);
+        ptr[i] += (long long)BK * ld;
+      }
+    } else {  // L_MC_CONV: k = output pixel, n = (tap, ci) fixed per chunk
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int y = poy[i] * g.st + ry[i], x = pox[i] * g.st + sx[i];
+        const bool v = ok[i] && pp[i] < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+        const T* src = base + (((long long)pim[i] * g.H + y) * g.W + x) * ld + cic[i];
+        glds16(v ? (const void*)src : zp, wbase + i * NT * 16);
+        // advance the pixel by one K tile
+        pp[i] += BK;
+        pox[i] += ax;
+        poy[i] += ay;
+        pim[i] += aim;
+        if (pox[i] >= g.OW) { pox[i] -= g.OW; poy[i] += 1; }
+        if (poy[i] >= g.OH) { poy[i] -= g.OH; pim[i] += 1; }
       }
     }
   }
@@ -371,8 +338,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
 
   LdA la;
   LdB lb;
-  la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid);
-  lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid);
+  la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid, kbeg);
+  lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid, kbeg);
 
   f32x4 acc[RM][RN];
 #pragma unroll
@@ -384,8 +351,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) {
     if (s < nt) {
-      la.issue(kbeg + s * BK, m0, tid, smem + s * STAGE);
-      lb.issue(kbeg + s * BK, n0, tid, smem + s * STAGE + ABYTES);
+      la.issue(kbeg + s * BK, smem + s * STAGE, tid);
+      lb.issue(kbeg + s * BK, smem + s * STAGE + ABYTES, tid);
     }
   }
   wait_tiles<G>(min(nt - 1, S - 2));
@@ -399,8 +366,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
   for (int kt = 0; kt < nt; ++kt) {
     if (kt + S - 1 < nt) {  // refill the stage consumed at kt-1 (all waves passed its barrier)
       char* dst = smem + nxt * STAGE;
-      la.issue(kbeg + (kt + S - 1) * BK, m0, tid, dst);
-      lb.issue(kbeg + (kt + S - 1) * BK, n0, tid, dst + ABYTES);
+      la.issue(kbeg + (kt + S - 1) * BK, dst, tid);
+      lb.issue(kbeg + (kt + S - 1) * BK, dst + ABYTES, tid);
     }
     const char* As = smem + cur * STAGE;
     const char* Bs = As + ABYTES;
