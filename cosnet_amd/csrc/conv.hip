@@ -101,9 +101,8 @@ extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, i
 
 
 // Weight-gradient plan: tile configuration and K split (M = Cout, N = KH*KW*Cin, K = pixels).
-// 256x256 tiles for the big ASPP-sized products, else 128x128 with 8 waves (128x64 for the
-// fp32 parity path); enough K splits to give ~2 blocks per CU (1 for the 256x256 tile, which
-// fills a CU's LDS), each split keeping >= 8 K tiles.
+// 128x128 tiles with 8 waves (128x64 for the fp32 parity path); enough K splits to give ~2
+// blocks per CU, each split keeping >= 8 K tiles.
 static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
                        int* chunk, int* cfg) {
   int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
@@ -111,8 +110,7 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
   long long tiles;
   int target = 512;
   if (dtype == DT_BF16) {
-    *cfg = (M >= 256 && NN >= 4096) ? 10 : 11;
-    if (*cfg == 10) target = 256;
+    *cfg = 11;  // 128x128, 8 waves: fastest for every wgrad shape of the step (tools/wgrad_sweep.sh)
     tiles = cn_gemm_cfg_blocks(*cfg, M, NN);
   } else {
     *cfg = -1;

@@ -19,6 +19,8 @@
 #include "common.h"
 #include "gemm.h"
 
+#include <type_traits>
+
 namespace {
 
 template <class T> struct Frag;
@@ -160,7 +162,8 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
           const int y = by[i] + oy, x = bx[i] + ox;
           const bool v = img[i] >= 0 && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
           ok[i] = v;
-          ptr[i] = base + (v ? (((long long)img[i] * g.H + y) * g.W + x) * ld : 0);
+          const unsigned pix = v ? (unsigned)((img[i] * g.H + y) * g.W + x) : 0u;
+          ptr[i] = base + (unsigned long long)pix * (unsigned long long)ld;
         }
         ctap = tap;
       }
@@ -180,7 +183,8 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
       for (int i = 0; i < NCH; ++i) {
         const int y = poy[i] * g.st + ry[i], x = pox[i] * g.st + sx[i];
         const bool v = ok[i] && pp[i] < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
-        const T* src = base + (((long long)pim[i] * g.H + y) * g.W + x) * ld + cic[i];
+        const unsigned pix = (unsigned)((pim[i] * g.H + y) * g.W + x);
+        const T* src = base + ((unsigned long long)pix * (unsigned long long)ld + (unsigned)cic[i]);
         glds16(v ? (const void*)src : zp, wbase + i * NT * 16);
         // advance the pixel by one K tile
         pp[i] += BK;
@@ -213,7 +217,7 @@ __device__ __forceinline__ bf16x8 read_frag_bf16(const char* lds, int rowbase, i
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
     typedef __attribute__((ext_vector_type(8))) short s16x8;
-    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, r);
   }
 }
@@ -361,16 +365,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
 #if CN_GEMM_PRIO == 2
   if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-  int cur = 0;                     // stage of tile kt
-  int nxt = S - 1;                 // stage of tile kt + S - 1
-  for (int kt = 0; kt < nt; ++kt) {
-    if (kt + S - 1 < nt) {  // refill the stage consumed at kt-1 (all waves passed its barrier)
-      char* dst = smem + nxt * STAGE;
-      la.issue(kbeg + (kt + S - 1) * BK, dst, tid);
-      lb.issue(kbeg + (kt + S - 1) * BK, dst + ABYTES, tid);
-    }
-    const char* As = smem + cur * STAGE;
-    const char* Bs = As + ABYTES;
+  auto mma_tile = [&](const char* As, const char* Bs) {
 #pragma unroll
     for (int pc = 0; pc < 2; ++pc) {
       if constexpr (sizeof(T) == 2) {
@@ -419,12 +414,57 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s4], bfr[j][s4], acc[i][j], 0, 0, 0);
       }
     }
+  };
+
+  // One K step on compile-time stage STG (tile kt lives in stage kt % S; the refill goes to the
+  // stage consumed one step earlier, which every wave has passed the barrier of).
+  auto kstep = [&](int kt, auto stg_c) {
+    constexpr int STG = decltype(stg_c)::value;
+    constexpr int NXT = (STG + S - 1) % S;
+    const char* As = smem + STG * STAGE;
+    const char* Bs = As + ABYTES;
+    if constexpr (sizeof(T) == 2 && (AMC || BMC) && (RM + RN) <= 8) {
+      // Transposed (MC) fragments are read with ds_read_b64_tr_b16, which hipcc cannot
+      // disambiguate from an in-flight LDS-DMA: a DMA issued before these reads would cost a
+      // full vmcnt(0) drain in front of them.  So read the whole tile's fragments FIRST, then
+      // issue the refill, then run the MFMAs on registers (tiles whose fragments fit in
+      // 64 VGPRs; the 256x256 tile keeps the refill-first order).
+      bf16x8 af[2][RM], bfr[2][RN];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[pc][i] = read_frag_bf16<BM, AMC>(As, wm * TM + i * 16, pc, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[pc][j] = read_frag_bf16<BN, BMC>(Bs, wn * TN + j * 16, pc, lane);
+      }
+      if (kt + S - 1 < nt) {
+        la.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE, tid);
+        lb.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE + ABYTES, tid);
+      }
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[pc][i], bfr[pc][j], acc[i][j], 0, 0, 0);
+    } else {
+      if (kt + S - 1 < nt) {
+        la.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE, tid);
+        lb.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE + ABYTES, tid);
+      }
+      mma_tile(As, Bs);
+    }
     // tile kt+1 must have landed (for every wave: counted wait, then the barrier); the
     // min(nt-1, kt+S-1) - (kt+1) younger tiles stay in flight
     wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
     raw_barrier();
-    cur = cur + 1 == S ? 0 : cur + 1;
-    nxt = nxt + 1 == S ? 0 : nxt + 1;
+  };
+  for (int kt = 0; kt < nt; kt += S) {
+    kstep(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nt) kstep(kt + 1, std::integral_constant<int, 1>{});
+    if constexpr (S > 2) { if (kt + 2 < nt) kstep(kt + 2, std::integral_constant<int, (S > 2 ? 2 : 0)>{}); }
+    if constexpr (S > 3) { if (kt + 3 < nt) kstep(kt + 3, std::integral_constant<int, (S > 3 ? 3 : 0)>{}); }
   }
 
   // Epilogue: stage alpha*acc (fp32) through LDS, HR tile rows per pass, as [HR][BN+4]; then
@@ -530,6 +570,10 @@ static constexpr TileCfg kCfg[] = {
     {256, 256, 4, 2, 2},  // 10
     {128, 128, 4, 2, 2},  // 11: 8 waves of 32x64
     {128, 64, 4, 2, 2},   // 12: 8 waves of 32x32
+    {128, 128, 4, 2, 3},  // 13: 8 waves, 3-deep ring
+    {128, 128, 4, 2, 4},  // 14: 8 waves, 4-deep ring
+    {256, 128, 4, 2, 3},  // 15
+    {128, 64, 4, 2, 4},   // 16
 };
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 static int g_force_cfg = -1;
@@ -586,6 +630,10 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 9: return launch_c<T, CT, 9, LA, LB>(a, batch, st);
       case 10: return launch_c<T, CT, 10, LA, LB>(a, batch, st);
       case 11: return launch_c<T, CT, 11, LA, LB>(a, batch, st);
+      case 13: return launch_c<T, CT, 13, LA, LB>(a, batch, st);
+      case 14: return launch_c<T, CT, 14, LA, LB>(a, batch, st);
+      case 15: return launch_c<T, CT, 15, LA, LB>(a, batch, st);
+      case 16: return launch_c<T, CT, 16, LA, LB>(a, batch, st);
       default: return launch_c<T, CT, 12, LA, LB>(a, batch, st);
     }
   }

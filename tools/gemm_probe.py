@@ -17,6 +17,10 @@ CONV = {  # n, cin, h, w, cout, k, stride, pad, dil
     "aspp": (8, 2048, 60, 60, 512, 3, 1, 12, 12),
     "l3": (8, 256, 60, 60, 256, 3, 1, 2, 2),
     "l3_1x1": (8, 1024, 60, 60, 256, 1, 1, 0, 1),
+    "l3b_1x1": (8, 256, 60, 60, 1024, 1, 1, 0, 1),
+    "l4": (8, 512, 60, 60, 512, 3, 1, 4, 4),
+    "l1": (8, 64, 119, 119, 64, 3, 1, 1, 1),
+    "l2": (8, 128, 60, 60, 128, 3, 1, 1, 1),
 }
 
 
@@ -33,7 +37,9 @@ def main():
         fl = 2.0 * m * n * k
         fn = lambda: ops.gemm(a, b, m, n, k, lda=k, ldb=k, out=c, ldc=n)  # noqa: E731
     else:
-        key, op = name.rsplit("_", 1) if name != "l3_1x1" else ("l3_1x1", "fwd")
+        key, op = name.rsplit("_", 1)
+        if op not in ("fwd", "dgrad", "wgrad"):
+            key, op = name, "fwd"
         n, cin, h, w, cout, kk, s, p, d = CONV[key]
         x = torch.randn(n * h * w, cin, device=dev).to(dt)
         wp = (torch.randn(cout, cin, kk, kk, device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
