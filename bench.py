@@ -24,6 +24,8 @@ sys.path.insert(0, REPO)
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
+PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_step_traffic.json")
 FLOP_PER_PAIR_473 = 4.1364e12    # SURVEY.md §8d (flop_counter on the reference graph)
 
 
@@ -39,6 +41,19 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     return ap.parse_args()
+
+
+def pmc_traffic(family):
+    """HBM traffic per launch of a kernel family from the committed rocprofv3 PMC summary
+    (tools/pmc_run.sh + tools/pmc_summary.py over this bench's own eager step)."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        e = dict(d["families"][family])
+        e["source"] = os.path.relpath(PMC_FILE, REPO) + ": " + d["source"]
+        return e
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(size):
@@ -174,15 +189,31 @@ def main():
         torch.cuda.synchronize()
     if prof:
         n, fl, kt = prof.summary()
+        nbytes = prof.algorithmic_bytes()
         if args.graph:  # one eager step: scale to the timed steps
-            n, fl, kt = n * args.steps, fl * args.steps, kt * args.steps
+            n, fl, kt, nbytes = n * args.steps, fl * args.steps, kt * args.steps, nbytes * args.steps
         peak = MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else MFMA_F32_PEAK_TFLOPS
         ach = fl / kt / 1e12
+        pmc = pmc_traffic("gemm_kernel")
         out["roofline"] = {"bound": "mfma", "kernel": "gemm_kernel (implicit-GEMM conv/bmm)",
                            "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-                           "traffic": None, "launches_per_step": n / args.steps,
+                           "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
+                           "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                           "traffic_source": pmc["source"] if pmc else None,
+                           "algorithmic_bytes_per_launch": nbytes / n,
+                           "launches_per_step": n / args.steps,
                            "gemm_time_frac_of_step": kt / dt,
                            "gemm_tflop_per_step": fl / args.steps / 1e12}
+        # the HW x HW affinity bmm S = (Va W^T) Vb^T (rgbd_segmentation_RAA.py:160,213): it writes
+        # the fp32 S to HBM, so its roofline is HBM bandwidth
+        an, afl, at, ab = prof.select("affinity")
+        if an:
+            out["roofline_affinity"] = {
+                "bound": "hbm", "kernel": "gemm_kernel, S = Va_t . Vb^T with fp32 S (B*HW x HW)",
+                "achieved": ab / at / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ab / at / 1e9 / HBM_PEAK_GBS, "tflops": afl / at / 1e12,
+                "mfma_frac": afl / at / 1e12 / peak, "launches_per_step": an / (1 if args.graph else args.steps),
+                "bytes_per_launch": ab / an, "us_per_launch": at / an * 1e6}
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if rank == 0 and args.cpu_baseline and world == 1:
         log("cpu baseline ...")

@@ -311,13 +311,17 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
   const int chunk = blockIdx.x * L.CB + tx;
   const bool on = chunk < L.CPR && ty < L.RPB;
   const int c0 = on ? chunk * V : 0;
-  float s1[V], s2[V], s3[V], mu[V], is[V], g[V], b[V];
+  float s1[V], s2[V], s3[V], mu[V], is[V], g[V], b[V], sc[V], sf[V];
   ld_params<V>(mean, c0, 0.f, mu);
   ld_params<V>(invstd, c0, 1.f, is);
   ld_params<V>(gamma, c0, 1.f, g);
   ld_params<V>(beta, c0, 0.f, b);
 #pragma unroll
-  for (int v = 0; v < V; ++v) s1[v] = s2[v] = s3[v] = 0.f;
+  for (int v = 0; v < V; ++v) {
+    s1[v] = s2[v] = s3[v] = 0.f;
+    sc[v] = g[v] * is[v];          // the forward apply's affine (bn_apply_k): the recomputed
+    sf[v] = b[v] - mu[v] * sc[v];  // ReLU mask (act 3) has exactly the forward's sign
+  }
   const float a = (act == 2) ? prelu[0] : 0.f;
   if (on) {
     const int step = gridDim.y * L.RPB;
@@ -337,6 +341,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
+          if (act == 3 && !(fmaf(xf[u][v], sc[v], sf[v]) > 0.f)) dd = 0.f;
           float xh = (xf[u][v] - mu[v]) * is[v];
           if (NQ > 2) {
             float pre = fmaf(xh, g[v], b[v]);
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
   if (chunk >= L.CPR || ty >= L.RPB) return;
-  float mu[V], is[V], k1[V], m1[V], m2[V], g[V], b[V];
+  float mu[V], is[V], k1[V], m1[V], m2[V], g[V], b[V], sf[V];
   const float invP = 1.f / (float)P;
   const int c0 = chunk * V;
   ld_params<V>(mean, c0, 0.f, mu);
@@ -394,6 +399,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     k1[v] = g[v] * is[v];
+    sf[v] = b[v] - mu[v] * k1[v];  // forward affine: mask of act 3 = fmaf(x, k1, sf) > 0
     m1[v] *= invP;
     m2[v] *= invP;
   }
@@ -417,6 +423,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
+        if (act == 3 && !(fmaf(xf[u][v], k1[v], sf[v]) > 0.f)) dd = 0.f;
         float xh = (xf[u][v] - mu[v]) * is[v];
         if (act == 2) {
           float pre = fmaf(xh, g[v], b[v]);

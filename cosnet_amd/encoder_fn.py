@@ -76,7 +76,7 @@ def stem_bwd(item, dout, grads):
     dy = torch.empty((pa, 64), dtype=dout.dtype, device=dout.device)
     nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n1, oh, ow, 64, ph,
             pw, 3, 2, 1, dy.data_ptr(), nv.stream())
-    dc, dg, db, _ = bn_bwd(c[:pa], dy, y[:pa], st[0], res.bn1, act=1)
+    dc, dg, db, _ = bn_bwd(c[:pa], dy, None, st[0], res.bn1, act=1)
     dw = conv_wgrad(x[:n1 * h * w], n1, h, w, 8, dc, oh, ow, 64, 7, 2, 3, 1)
     grads[res.conv1.weight] = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
     grads[res.bn1.weight] = dg
@@ -132,10 +132,10 @@ def bottleneck_bwd(item, dy, grads, need_dx=True):
         dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx)
     dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
     dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
-    dc2, dg2, db2, _ = bn_bwd(c2, dy2, y2, st2[0], blk.bn2, act=1)
+    dc2, dg2, db2, _ = bn_bwd(c2, dy2, None, st2[0], blk.bn2, act=1)
     dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
     dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
-    dc1, dg1, db1, _ = bn_bwd(c1, dy1, y1, st1[0], blk.bn1, act=1)
+    dc1, dg1, db1, _ = bn_bwd(c1, dy1, None, st1[0], blk.bn1, act=1)
     dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
     if need_dx:
         dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
@@ -211,7 +211,7 @@ def aspp_bwd(item, dout, grads):
     cms = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
     for bi, ((k, dd), ci, st, wt) in enumerate(zip(kd, cs, sts, wts)):
         sl = slice(512 * (bi + 1), 512 * (bi + 2))
-        dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], cat[:, sl], st[0], bns[bi], act=1)
+        dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], None, st[0], bns[bi], act=1)
         grads[cms[bi].weight] = as_param_grad(
             conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1)), cms[bi].weight)
         grads[cms[bi].bias] = ops.colsum(dci)
@@ -220,7 +220,7 @@ def aspp_bwd(item, dout, grads):
                         accumulate=dx is not None)
     dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
     ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
-    dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp[0], mod.bn_x, act=1)
+    dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp[0], mod.bn_x, act=1)
     grads[mod.conv.weight] = as_param_grad(conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1),
                                            mod.conv.weight)
     grads[mod.conv.bias] = ops.colsum(dcp)

@@ -66,7 +66,7 @@ class StemFn(F):
         dy = torch.empty_like(y)
         nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n, oh, ow, 64, ph,
                 pw, 3, 2, 1, dy.data_ptr(), nv.stream())
-        dc, dg, db, _ = bn_bwd(c, dy, y, st, ctx.mod.bn1, act=1)
+        dc, dg, db, _ = bn_bwd(c, dy, None, st, ctx.mod.bn1, act=1)
         dw = conv_wgrad(x, n, h, wd, 8, dc, oh, ow, 64, 7, 2, 3, 1)
         dw = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
         return None, None, dw, dg, db
@@ -126,10 +126,10 @@ class BottleneckFn(F):
             dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3, blk.bn3, act=1, dres=dx)
         dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
         dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
-        dc2, dg2, db2, _ = bn_bwd(c2, dy2, y2, st2, blk.bn2, act=1)
+        dc2, dg2, db2, _ = bn_bwd(c2, dy2, None, st2, blk.bn2, act=1)
         dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
         dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
-        dc1, dg1, db1, _ = bn_bwd(c1, dy1, y1, st1, blk.bn1, act=1)
+        dc1, dg1, db1, _ = bn_bwd(c1, dy1, None, st1, blk.bn1, act=1)
         dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
         dwd = None
         if need_dx:
@@ -209,7 +209,7 @@ class ASPPFn(F):
         bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
         for bi, ((k, dd), ci, st, wt) in enumerate(zip(ctx.convs, cs, sts, wts)):
             sl = slice(512 * (bi + 1), 512 * (bi + 2))
-            dci, dgi, dbi, _ = bn_bwd(ci, dcat[:, sl], cat[:, sl], st, bns[bi], act=1)
+            dci, dgi, dbi, _ = bn_bwd(ci, dcat[:, sl], None, st, bns[bi], act=1)
             dwi = conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1))
             dbias = ops.colsum(dci)
             if need_dx:
@@ -219,7 +219,7 @@ class ASPPFn(F):
         # image-pool branch: sum over HW of its cat slice
         dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
         ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
-        dcp, dgx, dbx, _ = bn_bwd(cp, dyp, yp, stp, mod.bn_x, act=1)
+        dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp, mod.bn_x, act=1)
         dwc = conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1)
         dbc = ops.colsum(dcp)
         if need_dx:
@@ -250,7 +250,7 @@ class CoattFn(F):
         vat = ops.gemm(va, wf, n * hw, c, c, lda=ops.ld(va), ldb=c)            # :158-159
         S = torch.empty((n, hw, ldp), dtype=torch.float32, device=dev)
         ops.gemm(vat, vb, hw, hw, c, lda=c, ldb=ops.ld(vb), a_bs=hw * c, b_bs=hw * ops.ld(vb),
-                 out=S, ldc=ldp, c_bs=hw * ldp, batch=n)                          # :160
+                 out=S, ldc=ldp, c_bs=hw * ldp, batch=n, tag="affinity")          # :160
         pc = torch.empty((n, hw, ldp), dtype=dt, device=dev)
         pt = torch.empty((n, hw, ldp), dtype=dt, device=dev)
         ws = torch.empty((int(nv.query("cn_coatt_workspace_floats", n, hw, ldp)),),

@@ -64,6 +64,12 @@ class GemmProfile:
         (the conv input tensor itself, not its implicit im2col) plus its output written once."""
         return sum(r[4] for r in self.rec)
 
+    def select(self, op):
+        """(launches, FLOPs, seconds, algorithmic bytes) of the launches whose tag op == `op`."""
+        sel = [r for r in self.rec if r[3] is not None and r[3][0] == op]
+        return (len(sel), sum(r[0] for r in sel),
+                sum(r[1].elapsed_time(r[2]) for r in sel) * 1e-3, sum(r[4] for r in sel))
+
     def by_tag(self):
         """{tag: [launches, FLOPs, seconds]} -- tag = (op, M, N, K) of each launch."""
         out = {}
@@ -245,7 +251,7 @@ GEMM_KC, GEMM_MC = 0, 2
 
 def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, a_bs=0, b_bs=0,
          out=None, ldc=None, c_bs=0, c_mode=0, batch=1, ka_lim=None, kb_lim=None, out_dtype=None,
-         nsplit=1, alpha=1.0, bias=None):
+         nsplit=1, alpha=1.0, bias=None, tag=None):
     """C[m, n] = alpha * sum_k A[m, k] * B[n, k] (batched via *_bs element strides)."""
     dt = a.dtype
     if out is None:
@@ -254,7 +260,7 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
         c_bs = m * n
     c_f32 = int(out.dtype == torch.float32)
     ev = _prof_start(2.0 * batch * m * n * (kb_lim if kb_lim is not None else k),
-                     ("gemm%d%d" % (layout_a, layout_b), batch * m, n, k),
+                     (tag or "gemm%d%d" % (layout_a, layout_b), batch * m, n, k),
                      (batch if a_bs else 1) * m * k * a.element_size() +
                      (batch if b_bs else 1) * n * k * b.element_size() +
                      batch * m * n * out.element_size())
@@ -349,8 +355,12 @@ def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rb
 
 
 def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=None):
-    """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu."""
+    """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu.
+    act=1 with y=None: the ReLU mask is recomputed from x with the forward's affine (no read of
+    the activation; only valid when y = relu(bn(x)) had no residual added)."""
     p, c = x.shape
+    if act == 1 and y is None:
+        act = 3
     dgamma = torch.empty((c,), dtype=torch.float32, device=x.device)
     dbeta = torch.empty_like(dgamma)
     dpc = torch.empty_like(dgamma) if act == 2 else None
