@@ -108,7 +108,11 @@ class TrainStep:
 
     def _after_pack(self):
         """world > 1: average the packed gradients and step SGD on them (eager, two calls)."""
-        dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+        if dist.get_backend(self.group) == "nccl":   # RCCL averages in the collective
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:                                           # gloo (CPU-side tests): no AVG op
+            dist.all_reduce(self.flat, group=self.group)
+            self.flat.mul_(1.0 / self.world)
         saved = [p.grad for p in self.params]
         for p, v in zip(self.params, self.views):
             if p.grad is not None:

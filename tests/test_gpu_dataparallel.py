@@ -1,0 +1,81 @@
+"""Data-parallel train step (cosnet_amd.train_step.TrainStep, world > 1) on the GPU.
+
+Two ranks share the box's one MI355X (gloo carries the collectives, RCCL cannot put two ranks
+on one device): each rank replays its captured HIP graph on its own frame pairs, the flat
+fp32 gradient buffer is averaged across ranks (train.py's DataParallel gradient reduce ->
+DDP semantics) and the SGD kernel steps every rank's masters from the SAME
+averaged gradient, so the parameters must stay bit-identical across ranks while the ranks'
+losses differ.  The BCE positive counts are all-reduced (global-batch weighting).
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import cosnet_amd as C
+    from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+    from cosnet_amd.optim import SGD, reference_param_groups
+    from cosnet_amd.train_step import TrainStep
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = C.build_model(torch.bfloat16)
+    m.load_state_dict(recipe_state_dict(m.state_dict()))
+    m.encoder.main_classifier.requires_grad_(False)
+    m = m.to(dev).train()
+    g0, g1 = reference_param_groups(m)
+    opt = SGD([g0, g1], [0.0, 0.0])
+    step = TrainStep(m, opt, 2, 65, graphed=True)
+    step.load(*[t.to(dev) for t in synthetic_inputs(2, 65, 65, seed=100 + rank)])
+    lrs = [2.5e-6, 2.5e-3]
+    opt.set_lrs(lrs)
+    step.capture(warmup=1)          # one eager data-parallel step, then the recorded graph
+    losses = [float(step.loss.item())]
+    for _ in range(2):
+        losses.append(float(step(lrs).item()))
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().float().flatten() for p in m.parameters()])
+    summary = torch.tensor([flat.double().sum().item(), flat.double().square().sum().item(),
+                            float(step.cnt[0].item()), float(step.cnt[1].item())] + losses,
+                           dtype=torch.float64)
+    torch.save({"summary": summary, "head": flat[:4096].cpu()},
+               os.path.join(outdir, "rank%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_graph_step_keeps_ranks_in_sync(cuda, tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [torch.load(os.path.join(str(tmp_path), "rank%d.pt" % i), weights_only=True) for i in range(world)]
+    s0, s1 = r[0]["summary"], r[1]["summary"]
+    # parameters identical on both ranks after 3 averaged-gradient steps
+    assert torch.equal(r[0]["head"], r[1]["head"])
+    assert s0[0] == s1[0] and s0[1] == s1[1]
+    # global positive counts are the same on both ranks (all-reduced)
+    assert s0[2] == s1[2] and s0[3] == s1[3]
+    # each rank trained on its own pairs: different losses, all finite
+    losses0, losses1 = s0[4:], s1[4:]
+    assert torch.isfinite(losses0).all() and torch.isfinite(losses1).all()
+    assert not torch.equal(losses0, losses1)
