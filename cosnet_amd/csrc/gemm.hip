@@ -163,7 +163,7 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
           const bool v = img[i] >= 0 && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
           ok[i] = v;
           const unsigned pix = v ? (unsigned)((img[i] * g.H + y) * g.W + x) : 0u;
-          ptr[i] = base + (unsigned long long)pix * (unsigned long long)ld;
+          ptr[i] = base + (unsigned long long)pix * (unsigned)ld;
         }
         ctap = tap;
       }
@@ -184,7 +184,7 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
         const int y = poy[i] * g.st + ry[i], x = pox[i] * g.st + sx[i];
         const bool v = ok[i] && pp[i] < klim && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
         const unsigned pix = (unsigned)((pim[i] * g.H + y) * g.W + x);
-        const T* src = base + ((unsigned long long)pix * (unsigned long long)ld + (unsigned)cic[i]);
+        const T* src = base + ((unsigned long long)pix * (unsigned)ld + (unsigned)cic[i]);
         glds16(v ? (const void*)src : zp, wbase + i * NT * 16);
         // advance the pixel by one K tile
         pp[i] += BK;
