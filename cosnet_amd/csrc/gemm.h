@@ -40,7 +40,7 @@ struct GemmArgs {
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);
 // Tile configuration the dispatcher picks for a bf16 problem, and its block count.
-int cn_gemm_pick(int M, int N, int batch_splits);
+int cn_gemm_pick(int M, int N, int K, int batch_splits);
 long long cn_gemm_cfg_blocks(int cfg, int M, int N);
 int cn_splitk_reduce_impl(const float* ws, int nsplit, long long slab, long long n, float* out,
                           int accumulate, hipStream_t st);

@@ -583,22 +583,21 @@ static long long cfg_blocks(int c, const GemmArgs& a, int batch) {
          batch * a.nsplit;
 }
 
-// Shape heuristic (tools/gemm_cfg_sweep.py on the step's conv shapes): 8-wave tiles win
-// everywhere except N <= 64; 256x256 once it still gives ~200+ blocks, 128x256 for N >= 256
-// at ~200+ blocks, 128x128 (8 waves of 32x64) otherwise.
-static int heuristic_cfg(int M, int N, int bz) {
-  GemmArgs a = {};
-  a.M = M; a.N = N; a.nsplit = 1;
+// Shape heuristic (tools/fwd_sweep.sh / wgrad_sweep.sh on the step's conv shapes, with the
+// K-invariant loaders): 256x256 for wide, deep products (N >= 512 and K >= 2048: the ASPP
+// atrous convs, layer-4, their dgrads) even below one block per CU; 128x64 for N <= 64;
+// 128x128 with 8 waves (32x64 per wave) everywhere else.
+static int heuristic_cfg(int M, int N, int K, int bz) {
+  (void)M; (void)bz;
   if (N <= 64) return 12;
-  if (N >= 512 && cfg_blocks(10, a, bz) >= 200) return 10;
-  if (N >= 256 && cfg_blocks(9, a, bz) >= 200) return 9;
+  if (N >= 512 && K >= 2048) return 10;
   return 11;
 }
 
 static int pick_cfg(const GemmArgs& a, int batch) {
   if (g_force_cfg >= 0 && g_force_cfg < kNumCfg) return g_force_cfg;
   if (a.cfg >= 0 && a.cfg < kNumCfg) return a.cfg;
-  return heuristic_cfg(a.M, a.N, batch * a.nsplit);
+  return heuristic_cfg(a.M, a.N, a.K, batch * a.nsplit);
 }
 
 template <class T, class CT, int C, int LA, int LB>
@@ -663,9 +662,9 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
   return -11;
 }
 
-int cn_gemm_pick(int M, int N, int batch_splits) {
+int cn_gemm_pick(int M, int N, int K, int batch_splits) {
   if (g_force_cfg >= 0 && g_force_cfg < kNumCfg) return g_force_cfg;
-  return heuristic_cfg(M, N, batch_splits);
+  return heuristic_cfg(M, N, K, batch_splits);
 }
 
 long long cn_gemm_cfg_blocks(int cfg, int M, int N) {

@@ -18,6 +18,16 @@ CONV = {  # n, cin, h, w, cout, k, stride, pad, dil
     "l3": (8, 256, 60, 60, 256, 3, 1, 2, 2),
     "l3_1x1": (8, 1024, 60, 60, 256, 1, 1, 0, 1),
     "l3b_1x1": (8, 256, 60, 60, 1024, 1, 1, 0, 1),
+    "l4_1x1": (8, 2048, 60, 60, 512, 1, 1, 0, 1),
+    "l4b_1x1": (8, 512, 60, 60, 2048, 1, 1, 0, 1),
+    "l1_1x1": (8, 256, 119, 119, 64, 1, 1, 0, 1),
+    "l1b_1x1": (8, 64, 119, 119, 256, 1, 1, 0, 1),
+    "l2_1x1": (8, 512, 60, 60, 128, 1, 1, 0, 1),
+    "l2b_1x1": (8, 128, 60, 60, 512, 1, 1, 0, 1),
+    "asppb": (8, 2560, 60, 60, 256, 3, 1, 1, 1),
+    "l3bd_1x1": (4, 256, 60, 60, 1024, 1, 1, 0, 1),
+    "l3d_1x1": (4, 1024, 60, 60, 256, 1, 1, 0, 1),
+    "l3d": (4, 256, 60, 60, 256, 3, 1, 2, 2),
     "l4": (8, 512, 60, 60, 512, 3, 1, 4, 4),
     "l1": (8, 64, 119, 119, 64, 3, 1, 1, 1),
     "l2": (8, 128, 60, 60, 128, 3, 1, 1, 1),
