@@ -103,15 +103,29 @@ extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, i
 // Weight-gradient plan: tile configuration and K split (M = Cout, N = KH*KW*Cin, K = pixels).
 // 128x128 tiles with 8 waves (128x64 for the fp32 parity path); enough K splits to give ~2
 // blocks per CU, each split keeping >= 8 K tiles.
+static int g_wgrad_target = 512;
+
+// Development hook (tuning tools only): blocks the wgrad K split aims for.
+extern "C" int cn_gemm_set_wgrad_target(int blocks) {
+  if (blocks < 1) return CN_ERR_SHAPE;
+  g_wgrad_target = blocks;
+  return 0;
+}
+
 static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
                        int* chunk, int* cfg) {
   int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
   int BK = 8 * vec_of(dtype);
   long long tiles;
-  int target = 512;
+  int target = g_wgrad_target;
   if (dtype == DT_BF16) {
-    *cfg = 11;  // 128x128, 8 waves: fastest for every wgrad shape of the step (tools/wgrad_sweep.sh)
+    // 128x128 / 8 waves (tools/wgrad_sweep.sh); the narrow layer-1 products get tiles that
+    // do not waste half their MFMAs: 128x64 for N <= 64, 64x128 for Cout <= 64
+    *cfg = NN <= 64 ? 12 : (M <= 64 ? 17 : 11);
     tiles = cn_gemm_cfg_blocks(*cfg, M, NN);
+    // split target from tools/wgrad_target_sweep.sh: many tiles (ASPP) -> 1024 blocks;
+    // wide Cout with few tiles (layer 3/4) -> 256 (longer K per split); narrow layers -> 512
+    if (target == 512) target = tiles >= 256 ? 1024 : (M >= 256 ? 256 : 512);
   } else {
     *cfg = -1;
     tiles = (long long)((M + 127) / 128) * ((NN + 63) / 64);

@@ -574,6 +574,7 @@ static constexpr TileCfg kCfg[] = {
     {128, 128, 4, 2, 4},  // 14: 8 waves, 4-deep ring
     {256, 128, 4, 2, 3},  // 15
     {128, 64, 4, 2, 4},   // 16
+    {64, 128, 2, 4, 2},   // 17: 8 waves of 32x32, for 64-row products (Cout = 64 wgrad)
 };
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 static int g_force_cfg = -1;
@@ -633,6 +634,7 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 14: return launch_c<T, CT, 14, LA, LB>(a, batch, st);
       case 15: return launch_c<T, CT, 15, LA, LB>(a, batch, st);
       case 16: return launch_c<T, CT, 16, LA, LB>(a, batch, st);
+      case 17: return launch_c<T, CT, 17, LA, LB>(a, batch, st);
       default: return launch_c<T, CT, 12, LA, LB>(a, batch, st);
     }
   }
@@ -680,28 +682,68 @@ extern "C" int cn_gemm_force_config(int cfg) {
   return kNumCfg;
 }
 
-// Split-K reduction: out[i] (+)= sum_s ws[s * slab + i]  (fp32, float4-vectorised, fixed order
-// so the result is bitwise reproducible).
-__global__ void splitk_reduce_k(const float* __restrict__ ws, int nsplit, long long slab,
-                                long long n4, float* __restrict__ out, int accumulate) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    f32x4 a = accumulate ? ((const f32x4*)out)[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < nsplit; ++s) {
-      f32x4 b = *(const f32x4*)(ws + s * slab + 4 * i);
-      a += b;
+// Split-K reduction: out[i] (+)= sum_s ws[s * slab + i]  (fp32, float4-vectorised).  A block
+// = (256 / G) float4 outputs x G slab groups: group g sums slabs g, g + G, ... (8 loads in
+// flight), then the G partials are added in group order through LDS -- a fixed order, so the
+// result is bitwise reproducible.  G grows when the output is small and the slabs many (the
+// layer-1 weight gradients: 16 K outputs x 110 slabs), so the chip is not left latency-bound.
+template <int G>
+__global__ __launch_bounds__(256) void splitk_reduce_k(const float* __restrict__ ws, int nsplit,
+                                                       long long slab, long long n4,
+                                                       float* __restrict__ out, int accumulate) {
+  constexpr int OPB = 256 / G;  // float4 outputs per block
+  __shared__ f32x4 red[G][OPB];
+  const int o = threadIdx.x % OPB, g = threadIdx.x / OPB;
+  for (long long base = (long long)blockIdx.x * OPB; base < n4; base += (long long)gridDim.x * OPB) {
+    const long long i = base + o;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+      int s = g;
+      for (; s + 7 * G < nsplit; s += 8 * G) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(ws + (long long)(s + u * G) * slab + 4 * i);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+      }
+      for (; s < nsplit; s += G) a += *(const f32x4*)(ws + (long long)s * slab + 4 * i);
     }
-    ((f32x4*)out)[i] = a;
+    if (G > 1) {
+      red[g][o] = a;
+      __syncthreads();
+      if (g == 0) {
+#pragma unroll
+        for (int q = 1; q < G; ++q) a += red[q][o];
+      }
+      __syncthreads();
+    }
+    if (g == 0 && i < n4) {
+      if (accumulate) a += ((const f32x4*)out)[i];
+      ((f32x4*)out)[i] = a;
+    }
   }
 }
 
 int cn_splitk_reduce_impl(const float* ws, int nsplit, long long slab, long long n, float* out,
                           int accumulate, hipStream_t st) {
   if (n % 4 || slab % 4) return -2;
-  long long n4 = n / 4;
-  long long b = (n4 + 255) / 256;
-  if (b > 2048) b = 2048;
-  hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)b), dim3(256), 0, st, ws, nsplit, slab, n4, out, accumulate);
+  const long long n4 = n / 4;
+  // slab groups: enough threads to cover the chip (~512 K), at most the number of slabs
+  int G = 1;
+  while (G < 16 && 2 * G <= nsplit && n4 * G < (512ll << 10)) G *= 2;
+  const int opb = 256 / G;
+  long long b = (n4 + opb - 1) / opb;
+  if (b > 4096) b = 4096;
+#define CN_RED(GG) \
+  hipLaunchKernelGGL(splitk_reduce_k<GG>, dim3((unsigned)b), dim3(256), 0, st, ws, nsplit, slab, n4, out, accumulate)
+  switch (G) {
+    case 1: CN_RED(1); break;
+    case 2: CN_RED(2); break;
+    case 4: CN_RED(4); break;
+    case 8: CN_RED(8); break;
+    default: CN_RED(16); break;
+  }
+#undef CN_RED
   CN_CHECK_LAUNCH();
   return 0;
 }

@@ -161,6 +161,8 @@ int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, 
 /* Development hook (tuning tools only): force GEMM tile configuration `cfg` for every bf16
  * launch; -1 restores the shape heuristic.  Returns the number of configurations. */
 int cn_gemm_force_config(int cfg);
+/* Development hook (tuning tools only): number of blocks the wgrad K split aims for. */
+int cn_gemm_set_wgrad_target(int blocks);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,15 @@ CONV = {  # n, cin, h, w, cout, k, stride, pad, dil
     "l3bd_1x1": (4, 256, 60, 60, 1024, 1, 1, 0, 1),
     "l3d_1x1": (4, 1024, 60, 60, 256, 1, 1, 0, 1),
     "l3d": (4, 256, 60, 60, 256, 3, 1, 2, 2),
+    "l1w": (4, 64, 119, 119, 64, 3, 1, 1, 1),
+    "l1w_1x1": (4, 256, 119, 119, 64, 1, 1, 0, 1),
+    "l1wb_1x1": (4, 64, 119, 119, 256, 1, 1, 0, 1),
+    "l2w_1x1": (4, 512, 60, 60, 128, 1, 1, 0, 1),
+    "l2wb_1x1": (4, 128, 60, 60, 512, 1, 1, 0, 1),
+    "l3w_1x1": (4, 1024, 60, 60, 256, 1, 1, 0, 1),
+    "l3wb_1x1": (4, 256, 60, 60, 1024, 1, 1, 0, 1),
+    "l3w": (4, 256, 60, 60, 256, 3, 1, 2, 2),
+    "asppw": (4, 2048, 60, 60, 512, 3, 1, 12, 12),
     "l4": (8, 512, 60, 60, 512, 3, 1, 4, 4),
     "l1": (8, 64, 119, 119, 64, 3, 1, 1, 1),
     "l2": (8, 128, 60, 60, 128, 3, 1, 1, 1),
@@ -39,6 +48,8 @@ def main():
     cfg = int(sys.argv[2]) if len(sys.argv) > 2 else -1
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 50
     nv.load().cn_gemm_force_config(cfg)
+    if len(sys.argv) > 4:
+        nv.load().cn_gemm_set_wgrad_target(int(sys.argv[4]))
     if name == "dense8k":
         m = n = k = 8192
         a = torch.randn(m, k, device=dev).to(dt)
