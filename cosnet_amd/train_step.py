@@ -158,6 +158,22 @@ class TrainStep:
             m._cn_nbt = k
         torch.cuda.synchronize()
 
+    def run_batch(self, rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b, lrs):
+        """One EAGER iteration on inputs of any size (the reference's augmented batches change
+        H, W every batch, so they cannot replay one recorded graph)."""
+        if self.graphed and self.graph is not None:
+            raise RuntimeError("run_batch is the eager path; build the TrainStep with graphed=False")
+        if self.world > 1 and self.flat is None:
+            self._flat_views()
+        b, _, h, w = rgb_a.shape
+        self.rgb_a, self.rgb_b, self.dep_a, self.dep_b, self.gt_a, self.gt_b = (
+            rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b)
+        self.hw = (h, w)
+        self.total = b * h * w * self.world
+        self.opt.set_lrs(lrs)
+        self._eager_once()
+        return self.loss
+
     def eager(self, lrs):
         """One eager (un-graphed) iteration, e.g. to time its kernels with HIP events."""
         self.opt.set_lrs(lrs)

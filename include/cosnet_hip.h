@@ -158,6 +158,14 @@ int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
               float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C, void* y,
               long long ldy, int accumulate, hipStream_t stream);
+/* ---- SBM-RGBD frame preparation (dataloaders/sbm_rgbd_loader.py:590-697, utils.py:5-55) -- */
+/* dst[c][H][W] (fp32) = cv2.resize(src window - mean[c]) with mode 0 INTER_LINEAR / 1
+ * INTER_NEAREST, horizontally flipped if flip; src element (c, y, x) of the window at
+ * src + c*plane_stride + (y0+y)*row_stride + (x0+x)*col_stride (uint8 if src_u8, else fp32). */
+int cn_frame_resize(int src_u8, const void* src, int C, long long plane_stride, long long row_stride,
+                    long long col_stride, int y0, int x0, int h, int w, const float* mean,
+                    float* dst, int H, int W, int mode, int flip, hipStream_t stream);
+
 /* Development hook (tuning tools only): force GEMM tile configuration `cfg` for every bf16
  * launch; -1 restores the shape heuristic.  Returns the number of configurations. */
 int cn_gemm_force_config(int cfg);

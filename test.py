@@ -12,6 +12,7 @@ MI355X-native: the N references run as ONE batched forward with the target encod
 (cosnet_amd.inference.multi_reference_x1; equal to the reference's loop in eval mode), the
 average and the resize are HIP kernels; only the uint8 masks cross to the host.  Checkpoints
 load with torch.load(weights_only=True); "module." prefixes are stripped (test.py:140-161).
+`--dataset sbmrgbd` reads the SBM-RGBD tree (cosnet_amd/sbm_rgbd.py, GPU frame preparation);
 `--dataset synthetic` evaluates seeded frame pairs (cosnet_amd/data.py).
 """
 import argparse
@@ -62,6 +63,7 @@ def config(args, user_config):
     w, h = map(int, str(ds["output_WH"]).split(","))
     args.output_WH = (w, h)
     args.frames = args.frames if args.frames is not None else int(ds.get("frames", 8))
+    args.subset = ds.get("subset") or None
 
 
 def main(argv=None):
@@ -106,11 +108,20 @@ def main(argv=None):
     model.eval()
     model.to(dev)
 
-    if args.dataset != "synthetic":
-        raise SystemExit("dataset %r: the SBM-RGBD / HzFu file loaders are not part of this build; "
-                         "use --dataset synthetic" % args.dataset)
-    db = SyntheticRGBDPairs(args.frames // args.batch_size, args.image_HW_4_model, args.batch_size,
-                            sample_range=args.sample_range, seed=4321)
+    if args.dataset == "sbmrgbd":
+        from cosnet_amd.sbm_rgbd import SBMRGBD
+        if not args.data_path or not os.path.isdir(args.data_path):
+            raise SystemExit("sbmrgbd: data_path %r not found (config.yaml test.dataset.sbmrgbd)" % args.data_path)
+        sbm = SBMRGBD(args.data_path, args.sample_range, args.image_HW_4_model, for_training=False,
+                      batch_size=args.batch_size, subset_percentage=1, subset=args.subset or None,
+                      device=dev)  # test.py:271-272
+        db = [sbm.collate([sbm[j] for j in range(i, i + args.batch_size)])
+              for i in range(0, len(sbm), args.batch_size)]
+    elif args.dataset == "synthetic":
+        db = SyntheticRGBDPairs(args.frames // args.batch_size, args.image_HW_4_model, args.batch_size,
+                                sample_range=args.sample_range, seed=4321)
+    else:
+        raise SystemExit("dataset %r: only sbmrgbd and synthetic are provided by this build" % args.dataset)
     out_dir = None
     if str(args.save_seg_img) not in ("False", "0", ""):
         out_dir = os.path.join(args.result_dir, "obj_seg_imgs")
@@ -126,7 +137,7 @@ def main(argv=None):
             sdep = torch.cat([batch["search_%d_depth" % i][j:j + 1] for i in range(args.sample_range)]).to(dev)
             x1 = multi_reference_x1(model, tgt, tdep, srch, sdep)          # [1,1,h,w]
             mask = masks_uint8(resize_linear(x1, out_hw))[0, 0]            # [H,W] uint8
-            gt = batch["target_gt"][j:j + 1].unsqueeze(1)
+            gt = batch["target_gt"][j:j + 1].unsqueeze(1).float().cpu()
             if tuple(gt.shape[2:]) != out_hw:
                 gt = torch.nn.functional.interpolate(gt, size=out_hw, mode="nearest")
             gt = gt[0, 0].numpy().astype(np.uint8)

@@ -50,7 +50,16 @@ def main():
     nv.load().cn_gemm_force_config(cfg)
     if len(sys.argv) > 4:
         nv.load().cn_gemm_set_wgrad_target(int(sys.argv[4]))
-    if name == "dense8k":
+    if name == "affinity":  # S = Va_t Vb^T per pair, fp32 S (CoattFn.forward)
+        nb, hw, c = 4, 3600, 256
+        ldp = (hw + 7) // 8 * 8
+        a = torch.randn(nb * hw, c, device=dev).to(dt)
+        b = torch.randn(nb * hw, c, device=dev).to(dt)
+        S = torch.empty((nb, hw, ldp), dtype=torch.float32, device=dev)
+        fl = 2.0 * nb * hw * hw * c
+        fn = lambda: ops.gemm(a, b, hw, hw, c, lda=c, ldb=c, a_bs=hw * c, b_bs=hw * c, out=S,  # noqa: E731
+                              ldc=ldp, c_bs=hw * ldp, batch=nb)
+    elif name == "dense8k":
         m = n = k = 8192
         a = torch.randn(m, k, device=dev).to(dt)
         b = torch.randn(n, k, device=dev).to(dt)

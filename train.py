@@ -16,8 +16,10 @@ MI355X-native differences:
   (config batch_size) is split over the ranks like DataParallel's scatter, BN statistics
   stay per device, the BCE positive count is all-reduced (global-batch semantics) and
   gradients are averaged with one flat all-reduce;
-* `--dataset synthetic` feeds seeded frame pairs (cosnet_amd/data.py); the SBM-RGBD file
-  loader (dataloaders/sbm_rgbd_loader.py) is outside this build's scope.
+* `--dataset sbmrgbd` reads the SBM-RGBD tree with the reference loader's rules, frame
+  preparation on the GPU (cosnet_amd/sbm_rgbd.py); its batches change size every iteration,
+  so those steps run eagerly.  `--dataset synthetic` feeds seeded frame pairs
+  (cosnet_amd/data.py) through the recorded-graph step.
 Extra flags: --config, --dtype (bf16 default; fp32 = the reference's arithmetic),
 --max-epoches / --iters-per-epoch (override config), --graph 0 (eager), --duplicate-params
 (the reference's repeated group-0 entries), --snapshot-root.
@@ -99,6 +101,7 @@ def configure_dataset_init_model(args, user_config, stamp):
                      else ds.get("iterations_per_epoch", 0) or 0)
     args.snapshot_dir = os.path.join(args.snapshot_root, "snapshots", args.dataset,
                                      args.full_model_name, "H%dW%d" % (h, w), stamp)
+    args.subset = ds.get("subset") or None
 
 
 def _free_port():
@@ -121,13 +124,44 @@ def _relaunch_data_parallel(args, argv):
     return subprocess.call(cmd, env=env)
 
 
-def make_dataset(args, per_rank_batch, rank):
+def make_dataset(args, per_rank_batch, rank, dev):
     from cosnet_amd.data import SyntheticRGBDPairs
     if args.dataset == "synthetic":
         return SyntheticRGBDPairs(args.iters or 4, args.output_HW, per_rank_batch,
                                   seed=args.random_seed + 7919 * rank, img_mean=args.img_mean)
-    raise SystemExit("dataset %r: the SBM-RGBD / HzFu file loaders (dataloaders/*.py) are not part "
-                     "of this build; use --dataset synthetic" % args.dataset)
+    if args.dataset == "sbmrgbd":
+        from cosnet_amd.sbm_rgbd import SBMRGBD
+        if not args.data_dir or not os.path.isdir(args.data_dir):
+            raise SystemExit("sbmrgbd: data_path %r not found (config.yaml train.dataset.sbmrgbd)" % args.data_dir)
+        return SBMRGBD(args.data_dir, 1, args.output_HW, for_training=True, batch_size=args.batch_size,
+                       subset=args.subset or None, meanval=args.img_mean, seed=args.random_seed,
+                       device=dev)
+    raise SystemExit("dataset %r: only sbmrgbd and synthetic are provided by this build" % args.dataset)
+
+
+class _SbmBatches:
+    """Shuffled global batches of the SBM-RGBD dataset, this rank's share of each (the
+    DataLoader(shuffle=True) + DataParallel scatter of train.py:533-534, :591).  Every rank draws
+    the same permutation and crop / scale ratios (same seed), so the ranks' frames have one size."""
+
+    def __init__(self, db, global_batch, rank, world, seed):
+        import random as _random
+        self.db, self.B, self.rank, self.world = db, global_batch, rank, world
+        self.rng = _random.Random(seed)
+        self.perm = list(range(len(db)))
+
+    def __len__(self):
+        return len(self.db) // self.B
+
+    def epoch(self, e):
+        self.rng.seed(e * 1000003 + 17)
+        self.rng.shuffle(self.perm)
+
+    def __getitem__(self, i):
+        self.db._scale_ratio = self.rng.uniform(0.7, 1.3)   # next_batch (:700-702)
+        self.db._crop_ratio = self.rng.uniform(0.8, 1)
+        idx = self.perm[i * self.B:(i + 1) * self.B][self.rank::self.world]
+        return self.db.collate([self.db[j] for j in idx])
 
 
 def main(argv=None):
@@ -215,30 +249,40 @@ def main(argv=None):
         logger.write("\n%s\t\t%s" % ("iter", "Loss(train)\n"))
         logger.flush()
 
-    db = make_dataset(args, per_rank, rank)
+    db = make_dataset(args, per_rank, rank, dev)
+    sbm = args.dataset == "sbmrgbd"
+    if sbm:  # augmented frames change size every batch: eager steps
+        db = _SbmBatches(db, args.batch_size, rank, world, args.random_seed)
     train_len = len(db)
     max_iter = args.maxEpoches * train_len
-    step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph))
+    step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph) and not sbm)
     say("=====> Begin to train: %d iterations per epoch, %d epochs, %d GPU(s) x %d pairs" % (
         train_len, args.maxEpoches, world, per_rank))
     t_start = time.time()
     loss_history = []
     captured = False
     for epoch in range(start_epoch, args.maxEpoches):
-        db.next_batch()
+        if sbm:
+            db.epoch(epoch)
+        else:
+            db.next_batch()
         for i_iter in range(train_len):
             batch = db[i_iter]
-            step.load(batch["target"].to(dev), batch["search_0"].to(dev),
-                      batch["target_depth"].to(dev), batch["search_0_depth"].to(dev),
-                      batch["target_gt"].unsqueeze(1).to(dev), batch["search_0_gt"].unsqueeze(1).to(dev))
             lr = lr_poly(args.learning_rate, i_iter + epoch * train_len, max_iter, args.power, epoch)
             lrs = [0.01 * lr, 10 * lr]  # train.py:171-172
-            if not captured:
+            ins = (batch["target"].to(dev), batch["search_0"].to(dev), batch["target_depth"].to(dev),
+                   batch["search_0_depth"].to(dev), batch["target_gt"].unsqueeze(1).to(dev).float(),
+                   batch["search_0_gt"].unsqueeze(1).to(dev).float())
+            if sbm:
+                loss = step.run_batch(*ins, lrs)
+            elif not captured:
+                step.load(*ins)
                 opt.set_lrs(lrs)
                 step.capture(warmup=1)  # this iteration runs eagerly, then the graph is recorded
                 captured = True
                 loss = step.loss
             else:
+                step.load(*ins)
                 loss = step(lrs)
             lv = float(loss.item())
             loss_history.append(lv)
