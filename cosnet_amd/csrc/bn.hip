@@ -18,6 +18,17 @@ constexpr int SUNR = 8;  // rows in flight per thread in the statistics pass
 struct Layout {
   int CPR, CB, RPB;
 };
+// Reduction passes (statistics, backward sums) use at most 32 chunk columns per block, so a
+// block walks >= 8 rows per step and wide layers (C = 1024..2560) need 8x fewer row splits:
+// the per-split partials (written by the pass, re-read by the finalize) stay ~2 MB instead of
+// ~17-25 MB per call.
+template <class T> __host__ __device__ inline Layout layout_red(int C) {
+  Layout l;
+  l.CPR = C / VecOf<T>::N;
+  l.CB = l.CPR < 32 ? l.CPR : 32;
+  l.RPB = 256 / l.CB;
+  return l;
+}
 template <class T> __host__ __device__ inline Layout layout_of(int C) {
   Layout l;
   l.CPR = C / VecOf<T>::N;
@@ -136,7 +147,7 @@ template <class T>
 __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x, long long ld, int P,
                                                         int C, float* __restrict__ ws) {
   constexpr int V = VecOf<T>::N;
-  const Layout L = layout_of<T>(C);
+  const Layout L = layout_red<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
   const int S = gridDim.y, seg = blockIdx.z;
@@ -306,7 +317,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
                                                        const float* beta, int act,
                                                        const float* prelu, float* __restrict__ ws) {
   constexpr int V = VecOf<T>::N;
-  const Layout L = layout_of<T>(C);
+  const Layout L = layout_red<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
   const bool on = chunk < L.CPR && ty < L.RPB;
@@ -441,8 +452,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
 // Row blocks for a launch: ~`blocks` blocks in total over gx x gy x nseg, each thread walking
 // >= min_rows rows.  Reductions use min_rows 8 (one statistics round) so the split count the
 // finalize has to sum stays small; streaming passes (apply) use UNR rows per thread.
-template <class T> int grid_rows(int P, int C, int* gx, int min_rows, int blocks, int nseg = 1) {
-  Layout L = layout_of<T>(C);
+template <class T> int grid_rows(int P, int C, int* gx, int min_rows, int blocks, int nseg = 1,
+                                 bool red = false) {
+  Layout L = red ? layout_red<T>(C) : layout_of<T>(C);
   *gx = (L.CPR + L.CB - 1) / L.CB;
   int want = (blocks / nseg + *gx - 1) / *gx;
   int maxy = (P + min_rows * L.RPB - 1) / (min_rows * L.RPB);
@@ -454,10 +466,10 @@ int g_tune[8] = {1024, SUNR, 2048, UNR, 1024, UNR, 2048, UNR};  // see cn_bn_set
 enum { T_ST_BLOCKS, T_ST_ROWS, T_AP_BLOCKS, T_AP_ROWS, T_BR_BLOCKS, T_BR_ROWS, T_BA_BLOCKS, T_BA_ROWS };
 
 template <class T> int stat_splits(int P, int C, int nseg, int* gx) {
-  return grid_rows<T>(P, C, gx, g_tune[T_ST_ROWS], g_tune[T_ST_BLOCKS], nseg);
+  return grid_rows<T>(P, C, gx, g_tune[T_ST_ROWS], g_tune[T_ST_BLOCKS], nseg, true);
 }
 template <class T> int bwd_splits(int P, int C, int* gx) {
-  return grid_rows<T>(P, C, gx, g_tune[T_BR_ROWS], g_tune[T_BR_BLOCKS]);
+  return grid_rows<T>(P, C, gx, g_tune[T_BR_ROWS], g_tune[T_BR_BLOCKS], 1, true);
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
