@@ -39,6 +39,7 @@ _SIGS = {
     "cn_coatt_workspace_floats": (_S, [_I, _I, _I]),
     "cn_coatt_softmax": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P]),
     "cn_coatt_dscore": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "cn_coatt_fused_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P]),
     "cn_nchw_to_nhwc": (_I, [_I, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cn_weight_prep": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cn_maxpool_fwd": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -1,0 +1,326 @@
+// Fused co-attention forward: both directions of the co-attention block without ever
+// materialising the HW x HW affinity (rgbd_segmentation_RAA.py:160-170 for RGB, :213-221 for
+// depth, inference / no-grad path):
+//
+//   S[i][j] = Va_t[i] . Vb[j]                                   (:160 / :213, bmm)
+//   Z_a[i]  = sum_j softmax_j(S[i][:])[j] * Vb[j]               (:165 + :170 -> "S_column")
+//   Z_b[j]  = sum_i softmax_i(S[:][j])[i] * Va[i]               (:164 + :169 -> "S_row")
+//
+// Both are the same "flash" product  O[q] = sum_k softmax_k(Q[q].K[k]) V[k]  (no temperature)
+// with (Q, K, V) = (Va_t, Vb, Vb) for Z_a and (Vb, Va_t, Va) for Z_b, so one kernel serves
+// both directions (blockIdx.z) and S is recomputed per direction on the MFMA instead of
+// written to HBM (51.8 MB fp32 per pair and modality at 473x473).
+//
+// Layout: pixel-major bf16 [B*HW][ld], channel dim D = 256 (all_channel).  One workgroup =
+// 4 waves = 128 query rows (32 per wave); key tiles of 64 rows stream through a 2-stage LDS
+// ring (K and V tile, 32 KB each per stage) filled by LDS-DMA.
+//   * "swapped" product S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 with Q held in registers as
+//     the B operand: the accumulator has the query row on the lane and 16 keys in registers,
+//     so the online-softmax row max / sum are lane-local (+ one xor-32 exchange for the max)
+//   * the accumulator, packed to bf16, is directly the B operand of O^T += V^T . P^T (its k
+//     order is the accumulator's row order); V^T fragments come from the [key][d] LDS image
+//     via the gfx950 transpose read ds_read_b64_tr_b16
+//   * K image: 16-B chunk XOR (key & 15) -> conflict-free ds_read_b128; V image: chunk XOR
+//     ((key & 3) << 2) -> conflict-free transposed reads.  Swizzles are applied on the DMA
+//     source address, so the DMA writes stay lane-linear.
+//   * O is rescaled only when some row's running max grew (wave-uniform branch, exact).
+#include "common.h"
+#include "../../include/cosnet_hip.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int FD = 256;              // feature channels (all_channel)
+constexpr int FBQ = 128;             // query rows per workgroup
+constexpr int FBK = 32;              // keys per tile
+constexpr int FROWB = FD * 2;        // bytes per key row in LDS
+constexpr int FTILE = FBK * FROWB;   // 16 KB per K (or V) tile
+constexpr int FQB = FBQ * FROWB;     // 64 KB Q block
+constexpr int FSTAGES = 3;           // K/V ring depth (two tiles in flight behind the one read)
+constexpr int FDMA = 2 * FTILE / 4096;  // LDS-DMA instructions per thread per K/V tile
+#ifndef RESCALE_T
+#define RESCALE_T 8.0f
+#endif
+
+__device__ __attribute__((aligned(16))) unsigned g_zero16_fused[4];
+
+__device__ __forceinline__ void glds16f(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier_f() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct FusedDir {
+  const bf16* q; const bf16* k; const bf16* v; bf16* o;
+  long long ldq, ldk, ldv, ldo;
+};
+struct FusedArgs {
+  FusedDir dir[2];
+  int HW, ndir, nrb, nwork;
+};
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// wait until at most N LDS/SMEM operations are outstanding; `v` is threaded through so the
+// consumer of v cannot be scheduled above the wait
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float* f) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)f[j];
+  return r;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void coatt_fused_fwd_k(FusedArgs a) {
+  // [Q: 128 rows x 512 B][stage 0: K | V][stage 1: K | V][stage 2: K | V]   (64 + 3 x 32 KB)
+  __shared__ __attribute__((aligned(16))) char lds[FQB + FSTAGES * 2 * FTILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // XCD-aware work order: hardware places workgroup i on XCD i % 8, so give each XCD a
+  // contiguous run of the (batch, direction)-major work list -- the row blocks of one
+  // (batch, direction) then share its K/V stream (3.7 MB) in that XCD's 4 MB L2.
+  const int per_xcd = (a.nwork + 7) >> 3;
+  const int work = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  if (work >= a.nwork) return;
+  const int rb = work % a.nrb, bd = work / a.nrb;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const int HW = a.HW;
+  const long long b = bd / a.ndir;
+  const bf16* Q = d.q + b * HW * d.ldq;
+  const bf16* K = d.k + b * HW * d.ldk;
+  const bf16* V = d.v + b * HW * d.ldv;
+  const int q0 = rb * FBQ;
+  const int qrow = q0 + w * 32 + r;
+  const void* zp = (const void*)g_zero16_fused;
+  char* qlds = lds;
+
+  // Q block DMA: chunk p of the 4096-chunk image -> row p >> 5, position p & 31, source chunk
+  // position ^ (row & 15) (same swizzle as K: conflict-free ds_read_b128 of rows)
+#pragma unroll
+  for (int i = 0; i < FQB / 4096; ++i) {
+    const int p = i * 256 + tid;
+    const int row = p >> 5, cpos = p & 31;
+    const bool ok = q0 + row < HW;
+    const bf16* src = Q + (long long)(q0 + row) * d.ldq + ((cpos ^ (row & 15)) << 3);
+    glds16f(ok ? (const void*)src : zp, qlds + (i * 256 + (tid & ~63)) * 16);
+  }
+
+  // K/V tile DMA: chunk p = 256 i + tid of the 1024-chunk image -> key row p >> 5, position
+  // p & 31; the source chunk is the position XOR the image's swizzle.
+  auto issue = [&](int t, int stage) {
+    char* kb = lds + FQB + stage * 2 * FTILE;
+    char* vb = kb + FTILE;
+    const int key0 = t * FBK;
+#pragma unroll
+    for (int i = 0; i < FTILE / 4096; ++i) {
+      const int p = i * 256 + tid;
+      const int row = p >> 5, cpos = p & 31;
+      const int key = key0 + row;
+      const bool ok = key < HW;
+      const bf16* ks = K + (long long)key * d.ldk + ((cpos ^ (row & 15)) << 3);
+      const bf16* vs = V + (long long)key * d.ldv + ((cpos ^ ((row & 3) << 2)) << 3);
+      const int wb = (i * 256 + (tid & ~63)) * 16;
+      glds16f(ok ? (const void*)ks : zp, kb + wb);
+      glds16f(ok ? (const void*)vs : zp, vb + wb);
+    }
+  };
+
+  const int nt = (HW + FBK - 1) / FBK;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+
+  f32x16 o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY;  // running row max, log2 domain
+  float l = 0.f;        // partial row sum over this lane half's keys
+  const float L2E = 1.4426950408889634f;
+
+  // fragment geometry
+  const int sw = r & 15;                                   // row swizzle of Q / K images
+  const char* qrp = qlds + (w * 32 + r) * FROWB;           // this lane's Q row
+  const int G = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;  // transposed V reads
+
+  int st = 0, st2 = 2;  // stages of tiles t and t+2
+  for (int t = 0; t < nt; ++t) {
+    // tile t landed when at most the FDMA chunks of tile t+1 are still in flight
+    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(FDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_f();
+    // the stage of tile t+2 was last read in iteration t-1, which every wave has finished
+#ifndef CF_NO_DMA
+    if (t + 2 < nt) issue(t + 2, st2);
+#endif
+    const char* kb = lds + FQB + st * 2 * FTILE;
+    st = st == FSTAGES - 1 ? 0 : st + 1;
+    st2 = st2 == FSTAGES - 1 ? 0 : st2 + 1;
+    const char* vb = kb + FTILE;
+
+    // ---- S^T tile (32 keys x 32 query rows per wave) = K Q^T over 16 k-steps of d;
+    // both fragments come from LDS, read KPF steps ahead
+    f32x16 s = f32x16{};
+    {
+      constexpr int KPF = 3;
+      const char* krp = kb + r * FROWB;
+      bf16x8 kf[KPF], qf[KPF];
+#pragma unroll
+      for (int u = 0; u < KPF; ++u) {
+        const int c = ((2 * u + h) ^ sw) << 4;
+        kf[u] = *(const bf16x8*)(krp + c);
+        qf[u] = *(const bf16x8*)(qrp + c);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        const bf16x8 kc = kf[ks % KPF], qc = qf[ks % KPF];
+        if (ks + KPF < 16) {
+          const int c = ((2 * (ks + KPF) + h) ^ sw) << 4;
+          kf[ks % KPF] = *(const bf16x8*)(krp + c);
+          qf[ks % KPF] = *(const bf16x8*)(qrp + c);
+        }
+#ifndef CF_NO_S
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc, qc, s, 0, 0, 0);
+#else
+        s[ks] += (float)kc[0] * (float)qc[1];
+#endif
+      }
+      // keep the reads KPF steps ahead: initial reads, then {1 MFMA, 2 ds_read} per step
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * KPF, 0);
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (ks + KPF < 16) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+    }
+
+    // ---- online softmax over the keys (register i: key 32t + (i&3) + 8(i>>2) + 4h)
+    const int key0 = t * FBK;
+    if (key0 + FBK > HW) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (key0 + (i & 3) + 8 * (i >> 2) + 4 * h >= HW) s[i] = -INFINITY;
+    }
+    float mx = s[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx * L2E);
+    // lazy rescale: keep the stale max while no row's max grew by more than RESCALE_T (log2
+    // units), so P <= 2^RESCALE_T (fp32 O / l have the headroom; P's bf16 rounding is relative)
+    if (__builtin_amdgcn_ballot_w64(mnew > m + RESCALE_T) != 0) {
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);  // m = -inf: 0 (o, l are 0)
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      m = mnew;
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        pv[j] = __builtin_amdgcn_exp2f(fmaf(s[8 * s2 + j], L2E, -m));
+        l += pv[j];
+      }
+      pf[s2] = pack8(pv);
+    }
+
+    // ---- O^T += V^T P^T: k-step sk covers keys 16 sk .. +15 in the accumulator's k order;
+    // 16 (dt, sk) steps, V^T fragments read VPF steps ahead.  The transposed reads are inline
+    // asm with explicit lgkmcnt waits: hipcc cannot tell the ds_read_b64_tr_b16 builtin apart
+    // from the in-flight LDS-DMA of the NEXT tile (other stage) and would drain vmcnt(0) in
+    // front of it, exposing the whole DMA latency every tile.
+    {
+      const unsigned vrow = lds_addr(vb + (4 * h + q4) * FROWB);
+      auto vread = [&](int dt, int sk) {
+        const int g = 8 * dt + 4 * (G & 1) + pp;  // 8-byte granule of d = 32 dt + 16 (G&1) + 4 pp
+        const unsigned a1 = vrow + 16 * sk * FROWB + ((g ^ (q4 << 3)) << 3);
+        u32x2 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a1));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "n"(8 * FROWB));
+        u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+        return __builtin_bit_cast(bf16x8, v);
+      };
+      constexpr int VPF = 3;
+      bf16x8 vf[VPF];
+#pragma unroll
+      for (int u = 0; u < VPF; ++u) vf[u] = vread(u >> 1, u & 1);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        bf16x8 cur = vf[it % VPF];
+        if (it + VPF < 16) vf[it % VPF] = vread((it + VPF) >> 1, (it + VPF) & 1);
+        const int younger = 2 * (15 - it < VPF ? 15 - it : VPF);  // reads issued after cur's
+        if (younger >= 6) lgkm_wait<6>(cur);
+        else if (younger == 4) lgkm_wait<4>(cur);
+        else if (younger == 2) lgkm_wait<2>(cur);
+        else lgkm_wait<0>(cur);
+#ifndef CF_NO_PV
+        o[it >> 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, pf[it & 1], o[it >> 1], 0, 0, 0);
+#else
+        o[it >> 1][it] += (float)cur[0] * (float)pf[it & 1][1];
+#endif
+      }
+    }
+  }
+
+  // ---- epilogue: O[qrow][d] = o / l ; register i of d tile dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
+  l += __shfl_xor(l, 32, 64);
+  if (qrow < HW) {
+    const float inv = 1.f / l;
+    bf16* op = d.o + (b * HW + qrow) * d.ldo + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+        *(bf16x4*)(op + 32 * dt + 8 * c) = v;
+      }
+  }
+}
+
+}  // namespace
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                  const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                                  void* zb, long long ld_z, hipStream_t st) {
+  if (C != FD || B <= 0 || HW <= 0) return CN_ERR_SHAPE;
+  if (ld_vat % 8 || ld_va % 8 || ld_vb % 8 || ld_z % 4 || ld_vat < C || ld_va < C || ld_vb < C || ld_z < C)
+    return CN_ERR_ALIGN;
+  if (!aligned16(vat) || !aligned16(va) || !aligned16(vb) || ((uintptr_t)za & 7) || ((uintptr_t)zb & 7))
+    return CN_ERR_ALIGN;
+  FusedArgs a;
+  int nd = 0;
+  // direction 0: Z_a = softmax_j(S) Vb  (queries i: Va_t; keys j: Vb; values Vb)
+  if (za) a.dir[nd++] = FusedDir{(const bf16*)vat, (const bf16*)vb, (const bf16*)vb, (bf16*)za, ld_vat, ld_vb, ld_vb, ld_z};
+  // direction 1: Z_b = softmax_i(S)^T Va  (queries j: Vb; keys i: Va_t; values Va)
+  if (zb) a.dir[nd++] = FusedDir{(const bf16*)vb, (const bf16*)vat, (const bf16*)va, (bf16*)zb, ld_vb, ld_vat, ld_va, ld_z};
+  if (nd == 0) return CN_ERR_SHAPE;
+  a.HW = HW;
+  a.ndir = nd;
+  a.nrb = (HW + FBQ - 1) / FBQ;
+  a.nwork = a.nrb * B * nd;
+  dim3 grid(((a.nwork + 7) / 8) * 8);
+  hipLaunchKernelGGL(coatt_fused_fwd_k, grid, dim3(256), 0, st, a);
+  CN_CHECK_LAUNCH();
+  return 0;
+}

@@ -248,6 +248,14 @@ class CoattFn(F):
         ldp = (hw + 7) // 8 * 8
         wf, _ = WCACHE.get(wsim, dt, need_t=False)
         vat = ops.gemm(va, wf, n * hw, c, c, lda=ops.ld(va), ldb=c)            # :158-159
+        ctx.geo = (n, hw, c, ldp)
+        ctx.set_materialize_grads(False)
+        if not _need(ctx) and ops.coatt_fused_ok(dt, c, va, vb):
+            # inference: both directions in one flash-style launch, S never leaves the chip
+            za = torch.empty((n * hw, c), dtype=dt, device=dev)
+            zb = torch.empty((n * hw, c), dtype=dt, device=dev)
+            ops.coatt_fused(vat, va, vb, n, hw, za, zb)                          # :160-170
+            return za, zb
         S = torch.empty((n, hw, ldp), dtype=torch.float32, device=dev)
         ops.gemm(vat, vb, hw, hw, c, lda=c, ldb=ops.ld(vb), a_bs=hw * c, b_bs=hw * ops.ld(vb),
                  out=S, ldc=ldp, c_bs=hw * ldp, batch=n, tag="affinity")          # :160
@@ -264,8 +272,6 @@ class CoattFn(F):
                       a_bs=hw * ldp, b_bs=hw * ops.ld(va), batch=n, kb_lim=hw)    # :169
         if _need(ctx):
             ctx.s = (va, vb, wf, pc, pt, za, zb)
-        ctx.geo = (n, hw, c, ldp)
-        ctx.set_materialize_grads(False)
         return za, zb
 
     @staticmethod

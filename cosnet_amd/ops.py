@@ -283,6 +283,31 @@ def gemm(a, b, m, n, k, layout_a=GEMM_KC, layout_b=GEMM_KC, lda=None, ldb=None, 
     return out
 
 
+# ---- fused co-attention (inference) ----------------------------------------------------------
+import os as _os
+
+# COSNET_COATT_FUSED=0 keeps the materialised-S path for inference too (A/B, tests)
+COATT_FUSED = _os.environ.get("COSNET_COATT_FUSED", "1") != "0"
+
+
+def coatt_fused_ok(dt, c, va, vb):
+    """The fused kernel covers bf16, C = 256 and 16-byte aligned rows (every RAA call site)."""
+    return (COATT_FUSED and dt == torch.bfloat16 and c == 256 and ld(va) % 8 == 0
+            and ld(vb) % 8 == 0 and va.data_ptr() % 16 == 0 and vb.data_ptr() % 16 == 0)
+
+
+def coatt_fused(vat, va, vb, n, hw, za=None, zb=None):
+    """Z_a = softmax_j(S) Vb and Z_b = softmax_i(S)^T Va with S = vat vb^T, never materialised
+    (rgbd_segmentation_RAA.py:160-170).  Algorithmic work: 3 x 2 HW^2 C per pair."""
+    c = vat.shape[1]
+    ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_fused", n, hw, c),
+                     (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
+    nv.call("cn_coatt_fused_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
+            ld(vb), n, hw, c, nv.ptr(za), nv.ptr(zb), ld(za if za is not None else zb), nv.stream())
+    _prof_end(ev)
+    return za, zb
+
+
 def _nsplit_eff(k, nsplit, dt):
     """Number of splits cn_gemm really launches (chunks rounded up to whole K tiles)."""
     bk = 64 if dt == torch.bfloat16 else 32

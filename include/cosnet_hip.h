@@ -99,6 +99,14 @@ int cn_coatt_softmax(int dtype, const float* S, int B, int HW, int ld, void* Pc,
 int cn_coatt_dscore(int dtype, const void* Pc, const float* dPc, const float* d1, const void* PT,
                     const float* dPr, const float* d2, int B, int HW, int ld, void* dS,
                     hipStream_t stream);
+/* Fused inference forward of both co-attention directions, S never written to HBM:
+ *   za[i] = sum_j softmax_j(S[i][:]) vb[j],  zb[j] = sum_i softmax_i(S[:][j]) va[i],  S = vat vb^T
+ * Replaces rgbd_segmentation_RAA.py:160-170 (RGB) and :213-221 (depth) when no gradient is
+ * needed.  bf16 only, C == 256, [B*HW][ld] pixel-major, ld_vat/ld_va/ld_vb % 8 == 0 and 16-byte
+ * aligned bases; za or zb may be NULL (that direction is skipped). */
+int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                       const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                       long long ld_z, hipStream_t stream);
 
 /* ---- memory-bound helpers -------------------------------------------------------------- */
 int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* y,

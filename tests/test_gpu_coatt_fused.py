@@ -1,0 +1,115 @@
+"""Fused co-attention forward (cn_coatt_fused_fwd, S never materialised) against
+
+  * an fp64 restatement of rgbd_segmentation_RAA.py:160-170 on the same bf16-rounded inputs
+    (S = Va_t Vb^T, S_column = softmax_j, S_row = softmax_i, Z_a = Vb . S_col, Z_b = Va . S_row),
+  * the materialised-S HIP path (affinity GEMM + two-direction softmax + two gathers).
+
+The fused kernel rounds the softmax weights to bf16 before the P.V product (as the
+materialised bf16 path does), so the tolerance is 1.5e-2 of the output scale; the logits have
+std ~16 (unscaled, realistic for trained features) so the softmax is peaky.
+"""
+import pytest
+import torch
+
+from cosnet_amd import _native as nv
+from cosnet_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1.5e-2
+
+
+def ref64(vat, va, vb, n, hw):
+    """fp64 on the device (test oracle arithmetic, not the product path)."""
+    c = vat.shape[1]
+    qa = vat[:, :c].double().reshape(n, hw, c)
+    a = va[:, :c].double().reshape(n, hw, c)
+    b = vb[:, :c].double().reshape(n, hw, c)
+    S = qa @ b.transpose(1, 2)                    # [n, i, j]
+    za = torch.softmax(S, dim=2) @ b              # rows i: softmax over j
+    zb = torch.softmax(S, dim=1).transpose(1, 2) @ a
+    return za.reshape(n * hw, c), zb.reshape(n * hw, c)
+
+
+def make(n, hw, c, cuda, ld_extra=0, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    def t(s):
+        x = (torch.randn((n * hw, c + ld_extra), generator=g) * s).to(torch.bfloat16).to(cuda)
+        return x[:, ld_extra:] if ld_extra else x
+    # |S| std ~ scale^2 * sqrt(c): scale 0.5 -> ~4 ... 1.0 -> 16
+    return t(scale), t(scale), t(scale)
+
+
+def rel(got, ref):
+    return ((got.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-9)).item()
+
+
+@pytest.mark.parametrize("n,hw", [(1, 1), (2, 63), (2, 64), (1, 65), (2, 127), (2, 128), (2, 169),
+                                  (1, 300), (2, 1271), (1, 3600), (5, 3600)])
+def test_fused_vs_fp64(cuda, n, hw):
+    c = 256
+    vat, va, vb = make(n, hw, c, cuda, seed=hw)
+    za = torch.empty((n * hw, c), dtype=torch.bfloat16, device=cuda)
+    zb = torch.empty_like(za)
+    ops.coatt_fused(vat, va, vb, n, hw, za, zb)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(za.float()).all() and torch.isfinite(zb.float()).all()
+    ea, eb = rel(za, ra), rel(zb, rb)
+    assert ea <= TOL and eb <= TOL, (ea, eb)
+
+
+@pytest.mark.parametrize("scale", [0.25, 0.5, 1.0, 1.5])
+def test_fused_logit_scales(cuda, scale):
+    """From nearly uniform attention (S std ~1) to one-hot (std ~36): online rescale paths."""
+    n, hw, c = 2, 700, 256
+    vat, va, vb = make(n, hw, c, cuda, seed=7, scale=scale)
+    za = torch.empty((n * hw, c), dtype=torch.bfloat16, device=cuda)
+    zb = torch.empty_like(za)
+    ops.coatt_fused(vat, va, vb, n, hw, za, zb)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    torch.cuda.synchronize()
+    assert rel(za, ra) <= TOL and rel(zb, rb) <= TOL, (rel(za, ra), rel(zb, rb))
+
+
+def test_fused_strided_views_and_single_direction(cuda):
+    """Channel-slice views (row stride 512, as concat buffers hand them over) and a NULL output."""
+    n, hw, c = 2, 500, 256
+    vat, va, vb = make(n, hw, c, cuda, ld_extra=256, seed=3)
+    assert ops.ld(va) == 512 and va.data_ptr() % 16 == 0
+    za = torch.empty((n * hw, c), dtype=torch.bfloat16, device=cuda)
+    zb = torch.empty_like(za)
+    ops.coatt_fused(vat, va, vb, n, hw, za, zb)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    zb1 = torch.full_like(za, 7.0)
+    ops.coatt_fused(vat, va, vb, n, hw, None, zb1)
+    torch.cuda.synchronize()
+    assert rel(za, ra) <= TOL and rel(zb, rb) <= TOL
+    assert torch.equal(zb1, zb)
+
+
+def test_fused_rejects_bad_shapes(cuda):
+    n, hw = 1, 64
+    vat, va, vb = make(n, hw, 128, cuda)
+    za = torch.empty((n * hw, 128), dtype=torch.bfloat16, device=cuda)
+    with pytest.raises(nv.NativeError):
+        ops.coatt_fused(vat, va, vb, n, hw, za, za)   # C != 256
+
+
+def test_coattfn_inference_uses_fused_and_matches_materialised(cuda, monkeypatch):
+    """CoattFn under no_grad goes through the fused kernel; same result as the materialised
+    HIP path (affinity GEMM + softmax kernels + gathers) within bf16 rounding of P."""
+    from cosnet_amd.functions import CoattFn
+    n, hw, c = 2, 3600, 256
+    _, va, vb = make(n, hw, c, cuda, seed=11, scale=0.7)
+    W = (torch.randn((c, c), generator=torch.Generator().manual_seed(5)) * c ** -0.5).to(cuda)
+    calls = []
+    real = ops.coatt_fused
+    monkeypatch.setattr(ops, "coatt_fused", lambda *a, **k: calls.append(1) or real(*a, **k))
+    with torch.no_grad():
+        fa, fb = CoattFn.apply(va, vb, W, (n, hw))
+        monkeypatch.setattr(ops, "COATT_FUSED", False)
+        ma, mb = CoattFn.apply(va, vb, W, (n, hw))
+    torch.cuda.synchronize()
+    assert len(calls) == 1
+    assert rel(fa, ma.double()) <= TOL and rel(fb, mb.double()) <= TOL, (rel(fa, ma.double()), rel(fb, mb.double()))
