@@ -60,3 +60,28 @@ def resize_linear(x, out_hw):
 def masks_uint8(x):
     """(output * 255).astype(np.uint8) of test.py:317 (truncation toward zero)."""
     return (x.detach().float().cpu().numpy() * 255).astype("uint8")
+
+
+@torch.no_grad()
+def soft_iou(x, gt):
+    """GPU quantisation + soft-J of test.py:317 / evaluation.py:3-22 (HIP kernel cn_soft_iou).
+
+    x: [n,1,H,W] (or [n,H,W]) fp32 in [0,1] on the GPU; gt: [n,H,W] {0,1} (any integer / bool /
+    float dtype holding 0/1; converted to uint8 like the reference's astype).
+    Returns (masks [n,H,W] uint8 on the GPU, iou [n] float64 on the GPU, counts [n,4] int64 =
+    (sum p&g, sum p|g, nonzero p, nonzero g)).  Bit-exact with evaluation.compute_iou on the
+    host masks."""
+    n = x.shape[0]
+    hw = x.shape[-2] * x.shape[-1]
+    if x.dtype != torch.float32 or not x.is_cuda:
+        raise RuntimeError("soft_iou: x must be fp32 on the GPU")
+    if gt.shape[0] != n or gt.shape[-2] * gt.shape[-1] != hw:
+        raise RuntimeError("soft_iou: gt %s does not match x %s" % (tuple(gt.shape), tuple(x.shape)))
+    x = x.contiguous()
+    g = gt.to(device=x.device, dtype=torch.uint8).contiguous()
+    masks = torch.empty((n,) + tuple(x.shape[-2:]), dtype=torch.uint8, device=x.device)
+    iou = torch.empty((n,), dtype=torch.float64, device=x.device)
+    counts = torch.empty((n, 4), dtype=torch.int64, device=x.device)
+    nv.call("cn_soft_iou", x.data_ptr(), g.data_ptr(), n, hw, masks.data_ptr(), iou.data_ptr(),
+            counts.data_ptr(), nv.stream())
+    return masks, iou, counts

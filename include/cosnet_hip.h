@@ -133,6 +133,11 @@ int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long 
                 float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 /* Mean of N stacked fp32 maps [N][C] -> [C] (N-reference average, test.py:287-305) */
 int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t stream);
+/* uint8 quantisation + soft-J per frame (test.py:317, evaluation.py:3-22): x [n][hw] fp32 in
+ * [0,1], gt [n][hw] uint8 {0,1} -> mask [n][hw] uint8 = trunc(255 x), iou[n] (double, bit-exact
+ * with numpy), counts[n][4] (optional) = {sum(p&g), sum(p|g), nonzero(p), nonzero(g)}. */
+int cn_soft_iou(const float* x, const unsigned char* gt, int nframes, long long hw,
+                unsigned char* mask, double* iou, long long* counts, hipStream_t stream);
 /* Workspace of the deterministic column reductions (gate/head backward, colsum). */
 size_t cn_colpart_workspace_floats(int P, int C);
 /* fusion + 1x1 classifier: rgbd_segmentation_RAA.py:251-261 ; deeplabv3_encoder.py:138 */

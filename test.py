@@ -76,8 +76,7 @@ def main(argv=None):
     import cosnet_amd as C
     from cosnet_amd.checkpoint import convert_state_dict, load_checkpoint
     from cosnet_amd.data import SyntheticRGBDPairs
-    from cosnet_amd.evaluation import compute_iou
-    from cosnet_amd.inference import masks_uint8, multi_reference_x1, resize_linear
+    from cosnet_amd.inference import multi_reference_x1, resize_linear, soft_iou
 
     with open(args.config) as f:
         user_config = yaml.safe_load(f)
@@ -136,12 +135,13 @@ def main(argv=None):
             srch = torch.cat([batch["search_%d" % i][j:j + 1] for i in range(args.sample_range)]).to(dev)
             sdep = torch.cat([batch["search_%d_depth" % i][j:j + 1] for i in range(args.sample_range)]).to(dev)
             x1 = multi_reference_x1(model, tgt, tdep, srch, sdep)          # [1,1,h,w]
-            mask = masks_uint8(resize_linear(x1, out_hw))[0, 0]            # [H,W] uint8
-            gt = batch["target_gt"][j:j + 1].unsqueeze(1).float().cpu()
+            gt = batch["target_gt"][j:j + 1].unsqueeze(1).float()
             if tuple(gt.shape[2:]) != out_hw:
                 gt = torch.nn.functional.interpolate(gt, size=out_hw, mode="nearest")
-            gt = gt[0, 0].numpy().astype(np.uint8)
-            iou = compute_iou(mask, gt)
+            # uint8 quantisation (:317) + soft-J (evaluation.py:3-22) in one HIP kernel
+            masks, ious, _ = soft_iou(resize_linear(x1, out_hw), gt[:, 0].to(torch.uint8).to(dev))
+            mask = masks[0].cpu().numpy()                                  # [H,W] uint8
+            iou = float(ious[0].item())
             seq, frame = batch["seq_name"][j], batch["frame_index"][j]
             logger.write(LOG_START + " seq: " + seq + " frame: " + frame + " IOU: " + str(iou) + LOG_END + "\n")
             iou_sum += iou
