@@ -84,6 +84,37 @@ def cpu_baseline(size):
                       "of the reference op sequence (oracle/model_ref.py); %.1f s" % (size, size, dt)}
 
 
+def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):
+    """Fused co-attention kernel (cn_coatt_fused_fwd: S = Va_t Vb^T, both softmax directions and
+    both gathers without materialising S) on the inference shape of BASELINE configs[3]: one
+    target + 5 reference frames at 473x473 -> n = 5 pairs of 60x60x256 bf16 features.
+    Algorithmic work 3 x 2 HW^2 C per pair (the kernel executes 4 x, S is
+    recomputed per direction), timed with HIP events on the launch stream."""
+    import torch
+    from cosnet_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(3)
+    vat, va, vb = [(torch.randn((n * hw, c), generator=g) * 0.7).to(torch.bfloat16).to(dev)
+                   for _ in range(3)]
+    za = torch.empty_like(va)
+    zb = torch.empty_like(va)
+    for _ in range(3):
+        ops.coatt_fused(vat, va, vb, n, hw, za, zb)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        ops.coatt_fused(vat, va, vb, n, hw, za, zb)
+    e1.record(s)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) * 1e-3 / iters
+    alg = 3 * 2.0 * n * hw * hw * c
+    return {"bound": "mfma", "kernel": "coatt_fused_fwd_k (flash-style, S never in HBM)",
+            "workload": "%d pairs x HW %d x C %d bf16 (configs[3]: 1 target + 5 refs, 473x473)" % (n, hw, c),
+            "achieved": alg / t / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": alg / t / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "executed_tflops": 4 / 3 * alg / t / 1e12, "us_per_launch": t * 1e6}
+
+
 def main():
     args = parse()
     import torch
@@ -215,6 +246,8 @@ def main():
                 "mfma_frac": afl / at / 1e12 / peak, "launches_per_step": an / (1 if args.graph else args.steps),
                 "bytes_per_launch": ab / an, "us_per_launch": at / an * 1e6}
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
+    if prof and dtype == torch.bfloat16 and S == 473:
+        out["roofline_coattention"] = coattention_roofline(dev)
     if rank == 0 and args.cpu_baseline and world == 1:
         log("cpu baseline ...")
         try:

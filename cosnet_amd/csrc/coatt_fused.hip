@@ -154,6 +154,9 @@ void coatt_fused_fwd_k(FusedArgs a) {
   const char* qrp = qlds + (w * 32 + r) * FROWB;           // this lane's Q row
   const int G = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;  // transposed V reads
 
+#ifdef CF_QREG
+  bf16x8 qreg[16];
+#endif
   int st = 0, st2 = 2;  // stages of tiles t and t+2
   for (int t = 0; t < nt; ++t) {
     // tile t landed when at most the FDMA chunks of tile t+1 are still in flight
@@ -172,23 +175,42 @@ void coatt_fused_fwd_k(FusedArgs a) {
     // ---- S^T tile (32 keys x 32 query rows per wave) = K Q^T over 16 k-steps of d;
     // both fragments come from LDS, read KPF steps ahead
     f32x16 s = f32x16{};
+#ifdef CF_QREG
+    // the wave's 32 query rows stay in registers (64 VGPRs) after the first tile: only the K
+    // fragments are read from LDS per tile
+    if (t == 0) {
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) qreg[ks] = *(const bf16x8*)(qrp + (((2 * ks + h) ^ sw) << 4));
+    }
+#endif
     {
       constexpr int KPF = 3;
       const char* krp = kb + r * FROWB;
-      bf16x8 kf[KPF], qf[KPF];
+      bf16x8 kf[KPF];
+#ifndef CF_QREG
+      bf16x8 qf[KPF];
+#endif
 #pragma unroll
       for (int u = 0; u < KPF; ++u) {
         const int c = ((2 * u + h) ^ sw) << 4;
         kf[u] = *(const bf16x8*)(krp + c);
+#ifndef CF_QREG
         qf[u] = *(const bf16x8*)(qrp + c);
+#endif
       }
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks) {
+#ifdef CF_QREG
+        const bf16x8 kc = kf[ks % KPF], qc = qreg[ks];
+#else
         const bf16x8 kc = kf[ks % KPF], qc = qf[ks % KPF];
+#endif
         if (ks + KPF < 16) {
           const int c = ((2 * (ks + KPF) + h) ^ sw) << 4;
           kf[ks % KPF] = *(const bf16x8*)(krp + c);
+#ifndef CF_QREG
           qf[ks % KPF] = *(const bf16x8*)(qrp + c);
+#endif
         }
 #ifndef CF_NO_S
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc, qc, s, 0, 0, 0);
@@ -196,12 +218,17 @@ void coatt_fused_fwd_k(FusedArgs a) {
         s[ks] += (float)kc[0] * (float)qc[1];
 #endif
       }
-      // keep the reads KPF steps ahead: initial reads, then {1 MFMA, 2 ds_read} per step
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * KPF, 0);
+      // keep the reads KPF steps ahead: initial reads, then {1 MFMA, NR ds_read} per step
+#ifdef CF_QREG
+      constexpr int NR = 1;
+#else
+      constexpr int NR = 2;
+#endif
+      __builtin_amdgcn_sched_group_barrier(0x100, NR * KPF, 0);
 #pragma unroll
       for (int ks = 0; ks < 16; ++ks) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (ks + KPF < 16) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        if (ks + KPF < 16) __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
       }
     }
 
