@@ -12,10 +12,9 @@
 // written to HBM (51.8 MB fp32 per pair and modality at 473x473).
 //
 // Layout: pixel-major bf16 [B*HW][ld], channel dim D = 256 (all_channel).  One workgroup =
-// 4 waves = 128 query rows (32 per wave); key tiles of 64 rows stream through a 2-stage LDS
-// ring (K and V tile, 32 KB each per stage) filled by LDS-DMA.
-//   * "swapped" product S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 with Q held in registers as
-//     the B operand: the accumulator has the query row on the lane and 16 keys in registers,
+// 4 waves = 128 query rows (32 per wave) held as a 64 KB LDS block; key tiles of 32 rows stream
+// through a 3-stage LDS ring (K and V tile, 16 KB each per stage) filled by LDS-DMA.
+//   * "swapped" product S^T = K . Q^T on v_mfma_f32_32x32x16_bf16 with Q as the B operand: the accumulator has the query row on the lane and 16 keys in registers,
 //     so the online-softmax row max / sum are lane-local (+ one xor-32 exchange for the max)
 //   * the accumulator, packed to bf16, is directly the B operand of O^T += V^T . P^T (its k
 //     order is the accumulator's row order); V^T fragments come from the [key][d] LDS image
@@ -39,6 +38,12 @@ constexpr int FTILE = FBK * FROWB;   // 16 KB per K (or V) tile
 constexpr int FQB = FBQ * FROWB;     // 64 KB Q block
 constexpr int FSTAGES = 3;           // K/V ring depth (two tiles in flight behind the one read)
 constexpr int FDMA = 2 * FTILE / 4096;  // LDS-DMA instructions per thread per K/V tile
+#ifndef CF_KPF
+#define CF_KPF 3  // K (and Q) fragment reads issued ahead of the S MFMAs
+#endif
+#ifndef CF_VPF
+#define CF_VPF 3  // V^T fragment reads issued ahead of the PV MFMAs (<= 7)
+#endif
 #ifndef RESCALE_T
 #define RESCALE_T 8.0f
 #endif
@@ -184,7 +189,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
     }
 #endif
     {
-      constexpr int KPF = 3;
+      constexpr int KPF = CF_KPF;
       const char* krp = kb + r * FROWB;
       bf16x8 kf[KPF];
 #ifndef CF_QREG
@@ -283,7 +288,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
         u32x4 v = {lo.x, lo.y, hi.x, hi.y};
         return __builtin_bit_cast(bf16x8, v);
       };
-      constexpr int VPF = 3;
+      constexpr int VPF = CF_VPF;
       bf16x8 vf[VPF];
 #pragma unroll
       for (int u = 0; u < VPF; ++u) vf[u] = vread(u >> 1, u & 1);
@@ -292,7 +297,11 @@ void coatt_fused_fwd_k(FusedArgs a) {
         bf16x8 cur = vf[it % VPF];
         if (it + VPF < 16) vf[it % VPF] = vread((it + VPF) >> 1, (it + VPF) & 1);
         const int younger = 2 * (15 - it < VPF ? 15 - it : VPF);  // reads issued after cur's
-        if (younger >= 6) lgkm_wait<6>(cur);
+        if (younger >= 14) lgkm_wait<14>(cur);
+        else if (younger == 12) lgkm_wait<12>(cur);
+        else if (younger == 10) lgkm_wait<10>(cur);
+        else if (younger == 8) lgkm_wait<8>(cur);
+        else if (younger == 6) lgkm_wait<6>(cur);
         else if (younger == 4) lgkm_wait<4>(cur);
         else if (younger == 2) lgkm_wait<2>(cur);
         else lgkm_wait<0>(cur);
