@@ -56,8 +56,25 @@ def pmc_traffic(family):
         return None
 
 
-def cpu_baseline(size):
-    """fp32 CPU oracle, B=2 train step (fwd + loss + bwd) at size x size."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(size, reps=3):
+    """The oracle's CPU restatement of the reference op sequence (fp32 torch CPU), timed on this
+    host on bounded samples, median of `reps` runs each:
+      train: one B=2 fwd+loss+bwd step at size x size (train mode needs B >= 2) -> the metric;
+      c1:    one eval forward of a 240x320 pair (BASELINE configs[0]);
+      c4:    test.py's N-reference loop (test.py:287-305): 5 eval forwards of the target with
+             one reference each at size x size, once (configs[3])."""
+    import statistics
     import torch
     from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
     import cosnet_amd as C
@@ -71,17 +88,46 @@ def cpu_baseline(size):
     threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
     torch.set_num_threads(threads)
     tmpl = C.build_model().state_dict()
-    ref = RefModel(recipe_state_dict(tmpl), dtype=torch.float32)
+    sd = recipe_state_dict(tmpl)
+    ref = RefModel(sd, dtype=torch.float32)
     ra, rb, da, db, ga, gb = synthetic_inputs(2, size, size, seed=99)
-    t0 = time.perf_counter()
-    x1, x2, _ = ref.forward(ra, rb, da, db)
-    loss = loss_bce_l1(x1, ga) + loss_bce_l1(x2, gb)
-    loss.backward()
-    dt = time.perf_counter() - t0
+    ts = []
+    for _ in range(reps):
+        for p in ref.p.values():
+            p.grad = None
+        t0 = time.perf_counter()
+        x1, x2, _ = ref.forward(ra, rb, da, db)
+        loss = loss_bce_l1(x1, ga) + loss_bce_l1(x2, gb)
+        loss.backward()
+        ts.append(time.perf_counter() - t0)
+    dt = statistics.median(ts)
+    evr = RefModel(sd, dtype=torch.float32, requires_grad=False)
+    evr.training = False
+    c1 = synthetic_inputs(1, 240, 320, seed=77)
+    t1 = []
+    with torch.no_grad():
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            evr.forward(*c1[:4])
+            t1.append(time.perf_counter() - t0)
+    n_ref = 5
+    q = synthetic_inputs(n_ref, size, size, seed=5)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        for i in range(n_ref):  # target re-encoded per reference, as test.py:287-293 does
+            evr.forward(q[0][:1], q[1][i:i + 1], q[2][:1], q[3][i:i + 1])
+        t4 = time.perf_counter() - t0
     return {"value": 2.0 / dt, "unit": "frame-pairs/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": "1 train step (fwd+loss+bwd), B=2 pairs at %dx%d, fp32 torch CPU restatement "
-                      "of the reference op sequence (oracle/model_ref.py); %.1f s" % (size, size, dt)}
+            "kind": "port", "cpu": _cpu_model(),
+            "sample": "median of %d train steps (fwd+loss+bwd), B=2 pairs at %dx%d, fp32 torch CPU "
+                      "restatement of the reference op sequence (oracle/model_ref.py): %s s" % (
+                          reps, size, size, ", ".join("%.2f" % t for t in ts)),
+            "c1_eval_240x320_pairs_per_s": 1.0 / statistics.median(t1),
+            "c1_sample": "median of %d eval forwards, 1 pair 240x320: %s s" % (
+                reps, ", ".join("%.2f" % t for t in t1)),
+            "c4_targets_per_s": 1.0 / t4,
+            "c4_sample": "test.py N-reference loop, 1 target x %d references at %dx%d (5 eval "
+                         "forwards): %.2f s" % (n_ref, size, size, t4)}
 
 
 def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):

@@ -255,11 +255,12 @@ __device__ __forceinline__ void block_partials(const float* acc, float accb, boo
     ws[(long long)gridDim.x * C + blockIdx.x] = (redb[0] + redb[1]) + (redb[2] + redb[3]);
 }
 
-// out[c] = scale * sum_{b < nb} part[b * C + c].  Block = 64 columns x 4 row groups; row group
-// w sums rows w, w+4, ... (4 loads in flight per step), then the 4 group sums are added in a
-// fixed order: deterministic.
+// out[c] = scale * sum_{b < nb} part[b * C + c] / div.  Block = 64 columns x 4 row groups; row
+// group w sums rows w, w+4, ... (4 loads in flight per step), then the 4 group sums are added in
+// a fixed order: deterministic.  (div: the N-reference mean divides like the reference's
+// `output_sum / sample_range`, test.py:305, instead of multiplying by a rounded 1/N.)
 __global__ __launch_bounds__(256) void colreduce_k(const float* __restrict__ part, int nb, int C,
-                                                   float scale, float* __restrict__ out) {
+                                                   float scale, float div, float* __restrict__ out) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + l;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(256) void colreduce_k(const float* __restrict__ par
   __shared__ float red[4][64];
   red[w][l] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (w == 0 && c < C) out[c] = ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) * scale;
+  if (w == 0 && c < C) out[c] = ((red[0][l] + red[1][l]) + (red[2][l] + red[3][l])) * scale / div;
 }
 
 template <class T>
@@ -840,15 +841,49 @@ extern "C" size_t cn_colpart_workspace_floats(int P, int C) {
 
 static int colreduce(const float* ws, int nb, int C, float* out, hipStream_t st) {
   if (!out) return 0;
-  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, ws, nb, C, 1.f, out);
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, ws, nb, C, 1.f, 1.f, out);
   CN_CHECK_LAUNCH();
   return 0;
 }
 
+// out[c] = (((x[0][c] + x[1][c]) + x[2][c]) + ...) / nrows: the reference's running fp32 sum
+// `output_sum += output` over the references followed by `/ sample_range` (test.py:301-305),
+// in the same order, so the mean is bit-identical given identical per-reference outputs.
+__global__ void mean_rows_seq_k(const float* __restrict__ x, int nrows, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = x[c];
+  for (int r = 1; r < nrows; ++r) s += x[(long long)r * C + c];
+  out[c] = s / (float)nrows;
+}
+
 extern "C" int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t st) {
   if (nrows < 1 || C < 1) return CN_ERR_SHAPE;
-  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, x, nrows, C,
-                     1.f / (float)nrows, out);
+  hipLaunchKernelGGL(mean_rows_seq_k, dim3((C + 255) / 256), dim3(256), 0, st, x, nrows, C, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_sum_rows(const float* x, int nrows, int C, float* out, hipStream_t st) {
+  if (nrows < 1 || C < 1) return CN_ERR_SHAPE;
+  hipLaunchKernelGGL(colreduce_k, dim3((C + 63) / 64), dim3(256), 0, st, x, nrows, C, 1.f, 1.f, out);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[i] = x[i] * s[0] (+ second tensor): the chain-rule scaling of a loss gradient by the
+// incoming device scalar, without a host read of it.
+__global__ void scale_dev_k(const float* __restrict__ x, long long n, const float* __restrict__ s,
+                            float* __restrict__ out) {
+  const float f = *s;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = x[i] * f;
+}
+
+extern "C" int cn_scale_dev(const float* x, long long n, const float* s, float* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scale_dev_k, dim3(nblocks(n)), dim3(256), 0, st, x, n, s, out);
   CN_CHECK_LAUNCH();
   return 0;
 }

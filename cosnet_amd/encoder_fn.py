@@ -18,7 +18,7 @@ from . import _native as nv
 from . import ops
 from .ops import WCACHE, as_param_grad, bn_apply, bn_bwd, bn_stats, conv_dgrad, conv_fwd, conv_wgrad
 
-F = torch.autograd.Function
+from .functions import F, _GRAD
 
 
 # ---- segment helpers -----------------------------------------------------------------------
@@ -239,7 +239,7 @@ class EncoderPairFn(F):
     @staticmethod
     def forward(ctx, img_a, img_b, enc, *params):
         dt = getattr(enc, "_cn_dtype", torch.bfloat16)
-        rec = [] if any(ctx.needs_input_grad[3:]) else None
+        rec = [] if (_GRAD[0] and any(ctx.needs_input_grad[3:])) else None
         nseg = 2
         x, geo = stem_fwd(enc.backbone, (img_a, img_b), nseg, dt, rec)
         for layer in (enc.backbone.layer1, enc.backbone.layer2, enc.backbone.layer3, enc.backbone.layer4):

@@ -20,11 +20,27 @@ from . import _native as nv
 from . import ops
 from .ops import WCACHE, bn_apply, bn_bwd, bn_stats, conv_dgrad, conv_fwd, conv_wgrad, as_param_grad
 
-F = torch.autograd.Function
+_GRAD = [True]  # grad mode of the caller of the innermost Function.apply in progress
+
+
+class F(torch.autograd.Function):
+    """autograd.Function that remembers the CALLER's grad mode: torch runs forward() under
+    no_grad and still reports needs_input_grad from each input's requires_grad (a Parameter
+    says True even inside torch.no_grad()), so `_need` must consult the outer mode to know
+    whether a backward can ever run (and e.g. pick the fused inference kernels)."""
+
+    @classmethod
+    def apply(cls, *args, **kwargs):
+        prev = _GRAD[0]
+        _GRAD[0] = torch.is_grad_enabled()
+        try:
+            return super().apply(*args, **kwargs)
+        finally:
+            _GRAD[0] = prev
 
 
 def _need(ctx):
-    return any(ctx.needs_input_grad)
+    return _GRAD[0] and any(ctx.needs_input_grad)
 
 
 def _check_train(ctx):
@@ -50,7 +66,7 @@ class StemFn(F):
         am = torch.empty((n * ph * pw * 64,), dtype=torch.uint8, device=img.device)
         nv.call("cn_maxpool_fwd", nv.dtype_code(dt), y.data_ptr(), n, oh, ow, 64, ph, pw, 3, 2, 1,
                 out.data_ptr(), am.data_ptr(), nv.stream())
-        if ctx.needs_input_grad[2]:
+        if _need(ctx):
             ctx.s = (x, c, y, am, st)
         ctx.geo = (n, cimg, h, wd, oh, ow, ph, pw)
         ctx.mod = mod
@@ -237,10 +253,15 @@ class ASPPFn(F):
 
 # ==============================================================================================
 class CoattFn(F):
-    """Z_a = softmax_j(S) V_b ; Z_b = softmax_i(S)^T V_a with S = (V_a W^T) V_b^T."""
+    """Z_a = softmax_j(S) V_b ; Z_b = softmax_i(S)^T V_a with S = (V_a W^T) V_b^T.
+
+    `link` (optional dict shared with the GateCatFn that concatenates V_a): that Function's
+    backward leaves its gradient for V_a in link["dv"] instead of returning it, and this
+    backward starts its dV_a accumulation from it, so V_a's two gradient contributions are
+    summed inside the HIP GEMM epilogues rather than by an autograd add."""
 
     @staticmethod
-    def forward(ctx, va, vb, wsim, geo):
+    def forward(ctx, va, vb, wsim, geo, link=None):
         n, hw = geo
         c = va.shape[1]
         dt = va.dtype
@@ -272,6 +293,7 @@ class CoattFn(F):
                       a_bs=hw * ldp, b_bs=hw * ops.ld(va), batch=n, kb_lim=hw)    # :169
         if _need(ctx):
             ctx.s = (va, vb, wf, pc, pt, za, zb)
+        ctx.link = link
         return za, zb
 
     @staticmethod
@@ -281,8 +303,9 @@ class CoattFn(F):
         dt = va.dtype
         dev = va.device
         P = n * hw
+        dv_link = ctx.link.pop("dv", None) if ctx.link is not None else None
         if dza is None and dzb is None:
-            return None, None, None, None
+            return dv_link, None, None, None, None
         dza = dza.contiguous() if dza is not None else None
         dzb = dzb.contiguous() if dzb is not None else None
         if dza is not None:
@@ -314,9 +337,13 @@ class CoattFn(F):
         if ctx.needs_input_grad[0]:
             dva = torch.empty((P, c), dtype=dt, device=dev)
             mode = 0
+            if dv_link is not None:  # the concat's gradient for V_a (GateCatFn, link)
+                ops.cast_copy(dv_link, dva)
+                mode = 2
             if dzb is not None:  # dVa += P_row . dZb  (A = P_row[i][j] = PT[j][i], MC layout)
                 ops.gemm(pt, dzb, hw, c, hw, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=ldp,
-                         ldb=c, a_bs=hw * ldp, b_bs=hw * c, out=dva, ldc=c, c_bs=hw * c, batch=n)
+                         ldb=c, a_bs=hw * ldp, b_bs=hw * c, out=dva, ldc=c, c_bs=hw * c, batch=n,
+                         c_mode=mode)
                 mode = 2
             # dVa += dVa_t . W   (B[n=ci][k=co] = W[co][ci] -> MC)
             ops.gemm(dvat, wf, P, c, c, layout_b=ops.GEMM_MC, lda=c, ldb=c, out=dva, ldc=c,
@@ -327,15 +354,17 @@ class CoattFn(F):
             ns = max(1, min(64, P // 512))
             ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
                      ldb=ops.ld(va), out=dw, ldc=c, c_mode=0, nsplit=ns)
-        return dva, None, dw, None
+        return dva, None, dw, None, None
 
 
 # ==============================================================================================
 class GateCatFn(F):
-    """out = cat([z * sigmoid(z.g + gb), v], 1); mask constant (no_grad) for the b side."""
+    """out = cat([z * sigmoid(z.g + gb), v], 1); mask constant (no_grad) for the b side.
+    With `link` (the dict given to the CoattFn that produced z from v), v's gradient is handed
+    to that CoattFn's backward through link["dv"] (see CoattFn)."""
 
     @staticmethod
-    def forward(ctx, z, v, g, gb, mask_const):
+    def forward(ctx, z, v, g, gb, mask_const, link=None):
         P, c = z.shape
         dt = z.dtype
         out = torch.empty((P, 2 * c), dtype=dt, device=z.device)
@@ -348,6 +377,7 @@ class GateCatFn(F):
             ctx.s = (z, mask, gflat)
         ctx.mask_const = mask_const
         ctx.has_gb = gb is not None
+        ctx.link = link
         return out
 
     @staticmethod
@@ -364,9 +394,12 @@ class GateCatFn(F):
                 ops.ld(dout), mask.data_ptr(), P, c, gflat.data_ptr(), int(through), dz.data_ptr(), c,
                 nv.ptr(dg), nv.ptr(dgb), nv.ptr(ws), nv.stream())
         dv = dout[:, c:] if ctx.needs_input_grad[1] else None
+        if dv is not None and ctx.link is not None:
+            ctx.link["dv"] = dv   # summed into dV_a by the producing CoattFn's backward
+            dv = None
         if dg is not None:
             dg = dg.view(1, c, 1, 1)
-        return dz, dv, dg, dgb, None
+        return dz, dv, dg, dgb, None, None
 
 
 class ConvFn(F):
@@ -472,6 +505,16 @@ class UpSigFn(F):
         return dl, None, None
 
 
+def _scaled(dpred, gout):
+    """dpred * gout with gout a device scalar (cn_scale_dev; no torch op, no host sync)."""
+    out = torch.empty_like(dpred)
+    g = gout.reshape(1).contiguous()
+    if g.dtype != torch.float32:
+        g = g.float()
+    nv.call("cn_scale_dev", dpred.data_ptr(), dpred.numel(), g.data_ptr(), out.data_ptr(), nv.stream())
+    return out
+
+
 class BceL1DevFn(F):
     """BceL1Fn with the BCE weight N*H*W / #pos taken from a device count tensor (int64 [1]):
     no host synchronisation, so the whole train step can be captured in a HIP graph."""
@@ -484,7 +527,7 @@ class BceL1DevFn(F):
         ws = torch.empty((int(nv.query("cn_loss_workspace_floats", n)),), dtype=torch.float32,
                          device=pred.device)
         loss = torch.empty((), dtype=torch.float32, device=pred.device)
-        dpred = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        dpred = torch.empty_like(pred) if _need(ctx) else None
         nv.call("cn_bce_l1_devcount", pred.data_ptr(), gt.data_ptr(), n, pos_count.data_ptr(),
                 float(total), float(l1w), ws.data_ptr(), loss.data_ptr(), nv.ptr(dpred), nv.stream())
         ctx.dpred = dpred
@@ -492,7 +535,38 @@ class BceL1DevFn(F):
 
     @staticmethod
     def backward(ctx, gout):
-        return ctx.dpred * gout, None, None, None, None
+        return _scaled(ctx.dpred, gout), None, None, None, None
+
+
+class BceL1PairDevFn(F):
+    """loss = BceL1(x1, gt_a) + BceL1(x2, gt_b) (train.py:595-597) in one Function: both
+    losses and their sum by HIP kernels, both weights from device counts [2] (no host sync)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, gt_a, gt_b, cnt, total, l1w):
+        two = torch.empty((2,), dtype=torch.float32, device=x1.device)
+        need = _need(ctx)
+        ds = []
+        for i, (pred, gt) in enumerate(((x1, gt_a), (x2, gt_b))):
+            pred = pred.contiguous()
+            gt = gt.contiguous()
+            n = pred.numel()
+            ws = torch.empty((int(nv.query("cn_loss_workspace_floats", n)),), dtype=torch.float32,
+                             device=pred.device)
+            dpred = torch.empty_like(pred) if need else None
+            nv.call("cn_bce_l1_devcount", pred.data_ptr(), gt.data_ptr(), n, cnt[i:i + 1].data_ptr(),
+                    float(total), float(l1w), ws.data_ptr(), two[i:i + 1].data_ptr(), nv.ptr(dpred),
+                    nv.stream())
+            ds.append(dpred)
+        loss = torch.empty((), dtype=torch.float32, device=x1.device)
+        nv.call("cn_sum_rows", two.data_ptr(), 2, 1, loss.data_ptr(), nv.stream())
+        ctx.ds = ds
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        da, db = ctx.ds
+        return _scaled(da, gout), _scaled(db, gout), None, None, None, None, None
 
 
 class BceL1Fn(F):
@@ -506,7 +580,7 @@ class BceL1Fn(F):
         ws = torch.empty((int(nv.query("cn_loss_workspace_floats", n)),), dtype=torch.float32,
                          device=pred.device)
         loss = torch.empty((), dtype=torch.float32, device=pred.device)
-        dpred = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        dpred = torch.empty_like(pred) if _need(ctx) else None
         nv.call("cn_bce_l1", pred.data_ptr(), gt.data_ptr(), n, float(weight), float(l1w),
                 ws.data_ptr(), loss.data_ptr(), nv.ptr(dpred), nv.stream())
         ctx.dpred = dpred
@@ -514,12 +588,12 @@ class BceL1Fn(F):
 
     @staticmethod
     def backward(ctx, gout):
-        return ctx.dpred * gout, None, None, None
+        return _scaled(ctx.dpred, gout), None, None, None
 
 
-def count_positive(gt):
-    """#(gt >= 0.5) on device (int64 tensor, no host sync)."""
-    cnt = torch.empty((1,), dtype=torch.int64, device=gt.device)
+def count_positive(gt, out=None):
+    """#(gt >= 0.5) on device (int64 tensor, no host sync), written into `out` if given."""
+    cnt = torch.empty((1,), dtype=torch.int64, device=gt.device) if out is None else out
     g = gt.contiguous()
     nv.call("cn_count_ge", g.data_ptr(), g.numel(), 0.5, cnt.data_ptr(), nv.stream())
     return cnt

@@ -399,8 +399,9 @@ def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=N
             nv.ptr(dx), ld(dx) if dx is not None else 0, nv.ptr(dres),
             ld(dres) if dres is not None else 0, ws.data_ptr(), nv.stream())
     dprelu = None
-    if dpc is not None:
-        dprelu = dpc.sum().reshape(1)  # C=256 floats -> 1 (tiny)
+    if dpc is not None:  # per-channel partials -> the single PReLU weight (fixed order)
+        dprelu = torch.empty((1,), dtype=torch.float32, device=x.device)
+        nv.call("cn_sum_rows", dpc.data_ptr(), c, 1, dprelu.data_ptr(), nv.stream())
     return dx, dgamma, dbeta, dprelu
 
 

@@ -173,16 +173,18 @@ class RGBDSegmentation_RAA(nn.Module):
         n, h, w = geo
         hw = h * w
         # RGB co-attention
-        za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw))
-        cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False)
+        link = {}   # V_a's two gradient contributions meet inside CoattFn's backward
+        za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw), link)
+        cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False, link)
         cat_b = fn.GateCatFn.apply(zb, vb, self.gate.weight, None, True)  # mask_b no_grad (:178-182)
         z_a = fn.BNFn.apply(fn.ConvFn.apply(cat_a, self.reduce_channels_A.weight, None, geo, 3, 1, 1, 1),
                             self.bn_A.weight, self.bn_A.bias, self.bn_A)
         z_b = fn.BNFn.apply(fn.ConvFn.apply(cat_b, self.reduce_channels_B.weight, None, geo, 3, 1, 1, 1),
                             self.bn_B.weight, self.bn_B.bias, self.bn_B)
         # depth co-attention
-        dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw))
-        dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False)
+        dlink = {}
+        dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw), dlink)
+        dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False, dlink)
         dz_a = fn.BNFn.apply(fn.ConvFn.apply(dcat_a, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
                              self.depth_bn.weight, self.depth_bn.bias, self.depth_bn)
         dz_a = fn.ConvFn.apply(dz_a, self.depth_weights.weight, self.depth_weights.bias, geo, 1, 1, 0, 1)

@@ -49,6 +49,12 @@ class TrainStep:
         self.cnt = torch.zeros((2,), dtype=torch.int64, device=dev)
         self.total = b * h * w * self.world
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
+        self.mem_hook = None   # callable(prefix): the reference's logMem (train.py:51-58)
+        self._capturing = False
+        # every eager iteration AND the capture run on this one stream: autograd pins each
+        # parameter's AccumulateGrad node to the stream it was created on
+        self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self.params = []
         seen = set()
         for g in opt.groups:
@@ -69,19 +75,36 @@ class TrainStep:
 
     def _counts(self):
         """Global #(gt >= 0.5) of both frames (train.py:183-187), before the graph."""
-        self.cnt[0:1].copy_(fn.count_positive(self.gt_a))
-        self.cnt[1:2].copy_(fn.count_positive(self.gt_b))
+        fn.count_positive(self.gt_a, out=self.cnt[0:1])
+        fn.count_positive(self.gt_b, out=self.cnt[1:2])
         if self.world > 1:
             dist.all_reduce(self.cnt, group=self.group)
+
+    def _mem(self, prefix):
+        if self.mem_hook is not None and not self._capturing:
+            self.mem_hook(prefix)
+
+    def _on_stream(self, fn_, *a):
+        """Run fn_ on self.stream (ordered after the caller's current stream and back)."""
+        if self.stream is None:
+            return fn_(*a)
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            r = fn_(*a)
+        cur.wait_stream(self.stream)
+        return r
 
     # ---- the recorded body -------------------------------------------------------------------
     def _body(self):
         self.opt.zero_grad()
         x1, x2, _ = self.model(self.rgb_a, self.rgb_b, self.dep_a, self.dep_b)
-        loss = (fn.BceL1DevFn.apply(x1, self.gt_a, self.cnt[0:1], self.total, self.l1) +
-                fn.BceL1DevFn.apply(x2, self.gt_b, self.cnt[1:2], self.total, self.l1))
-        loss.backward()
-        self.loss.copy_(loss.detach())
+        loss = fn.BceL1PairDevFn.apply(x1, x2, self.gt_a, self.gt_b, self.cnt, self.total, self.l1)
+        self._mem(" After forward")
+        # d loss / d loss = 1 from a preallocated device scalar (no fill kernel per step)
+        torch.autograd.backward(loss, self._one)
+        self._mem(" After backward")
+        self.loss = loss.detach()
         if self.world == 1:
             self.opt.step()
         else:
@@ -134,15 +157,13 @@ class TrainStep:
             for _ in range(warmup):
                 self._eager_once()
             return
-        # warm up AND record on one side stream: autograd pins each parameter's gradient
-        # accumulator to the stream it was created on, and an accumulation (a parameter used
-        # twice) running on any other stream than the capturing one would escape the graph
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                self._eager_once()
-        torch.cuda.current_stream().wait_stream(s)
+        # warm up AND record on one side stream (self.stream): autograd pins each parameter's
+        # gradient accumulator to the stream it was created on, and an accumulation (a
+        # parameter used twice) running on any other stream than the capturing one would
+        # escape the graph
+        s = self.stream
+        for _ in range(warmup):
+            self._eager_once()
         torch.cuda.synchronize()
         self.opt.reserve()
         self.opt.freeze_for_capture()
@@ -150,8 +171,13 @@ class TrainStep:
         torch.cuda.synchronize()
         before = self._bn_counts()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=s):
-            self._body()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(self.graph, stream=s):
+                self._body()
+        finally:
+            self._capturing = False
+        self._graph_loss = self.loss
         after = self._bn_counts()
         self._nbt_delta = {m: after[m] - before[m] for m in after if after[m] != before[m]}
         for m, k in before.items():  # recording executed nothing: only replays count
@@ -181,11 +207,13 @@ class TrainStep:
         return self.loss
 
     def _eager_once(self):
-        self._counts()
-        self.opt.refresh_lrs()
-        self._body()
-        if self.world > 1:
-            self._after_pack()
+        def once():
+            self._counts()
+            self.opt.refresh_lrs()
+            self._body()
+            if self.world > 1:
+                self._after_pack()
+        self._on_stream(once)
 
     def __call__(self, lrs):
         """One iteration on the loaded inputs with learning rates `lrs` (one per group)."""
@@ -196,6 +224,9 @@ class TrainStep:
         self.opt.refresh_lrs()
         self._counts()
         self.graph.replay()
+        self.loss = self._graph_loss
+        self._mem(" After forward")
+        self._mem(" After backward")
         # the replay updated the fp32 masters AND their compute-dtype copies in place (cn_sgd):
         # the weight cache stays valid
         for m, d in self._nbt_delta.items():

@@ -131,8 +131,15 @@ int cn_gate_bwd(int dtype, const void* z, long long ldz, const void* dout, long 
                 const float* mask, int P, int C, const float* g, int through_mask, void* dz,
                 long long lddz, float* dg, float* dgb,
                 float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
-/* Mean of N stacked fp32 maps [N][C] -> [C] (N-reference average, test.py:287-305) */
+/* Mean of N stacked fp32 maps [N][C] -> [C] (N-reference average, test.py:287-305): the fixed-
+ * order sum divided by N, like the reference's `output_sum / sample_range` (test.py:305). */
 int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t stream);
+/* Fixed-order column sums of [nrows][C] fp32 (e.g. the per-channel PReLU gradient partials of
+ * deeplab/deeplabv3_encoder.py:82 -> the single PReLU weight's gradient). */
+int cn_sum_rows(const float* x, int nrows, int C, float* out, hipStream_t stream);
+/* out[i] = x[i] * s[0], s a device scalar: chain rule of a loss gradient (autograd of
+ * train.py:595-599) without a host read. */
+int cn_scale_dev(const float* x, long long n, const float* s, float* out, hipStream_t stream);
 /* uint8 quantisation + soft-J per frame (test.py:317, evaluation.py:3-22): x [n][hw] fp32 in
  * [0,1], gt [n][hw] uint8 {0,1} -> mask [n][hw] uint8 = trunc(255 x), iou[n] (double, bit-exact
  * with numpy), counts[n][4] (optional) = {sum(p&g), sum(p|g), nonzero(p), nonzero(g)}. */

@@ -42,7 +42,8 @@ def get_arguments(argv=None):
     # this build
     p.add_argument("--config", default=os.path.join(REPO, "config.yaml"))
     p.add_argument("--checkpoint", default=None, help="overrides test.model.<name>.pretrained_params")
-    p.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="bf16 (default): the MI355X throughput path, fused co-attention; fp32: the reference arithmetic")
     p.add_argument("--result-root", default=".")
     p.add_argument("--frames", type=int, default=None, help="synthetic: number of target frames")
     return p.parse_args(argv)

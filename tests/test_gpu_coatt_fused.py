@@ -102,7 +102,8 @@ def test_coattfn_inference_uses_fused_and_matches_materialised(cuda, monkeypatch
     from cosnet_amd.functions import CoattFn
     n, hw, c = 2, 3600, 256
     _, va, vb = make(n, hw, c, cuda, seed=11, scale=0.7)
-    W = (torch.randn((c, c), generator=torch.Generator().manual_seed(5)) * c ** -0.5).to(cuda)
+    # an nn.Parameter like the model's similarity weight (requires_grad=True under no_grad)
+    W = torch.nn.Parameter((torch.randn((c, c), generator=torch.Generator().manual_seed(5)) * c ** -0.5).to(cuda))
     calls = []
     real = ops.coatt_fused
     monkeypatch.setattr(ops, "coatt_fused", lambda *a, **k: calls.append(1) or real(*a, **k))

@@ -26,6 +26,7 @@ Extra flags: --config, --dtype (bf16 default; fp32 = the reference's arithmetic)
 """
 import argparse
 import datetime
+import gc
 import os
 import socket
 import subprocess
@@ -63,7 +64,25 @@ def get_arguments(argv=None):
     p.add_argument("--graph", type=int, default=1)
     p.add_argument("--duplicate-params", action="store_true")
     p.add_argument("--snapshot-root", default=".")
+    p.add_argument("--log-mem", type=int, default=1,
+                   help="logMem lines around each iteration like train.py:560-621 (0: off)")
     return p.parse_args(argv)
+
+
+def log_mem(logger, prefix):
+    """logMem of train.py:51-58: allocated / reserved ("cached") device memory of this process's
+    GPU, printed and appended to the train log.  torch.cuda.memory_cached is gone from current
+    torch; memory_reserved is the same quantity (the caching allocator's pool)."""
+    import torch
+    total = torch.cuda.get_device_properties(None).total_memory
+    mem_alloc = torch.cuda.memory_allocated()
+    mem_cache = torch.cuda.memory_reserved()
+    msg = (prefix + " GPU: " + str(torch.cuda.current_device()) + " mem_alloc: " +
+           str(mem_alloc / 1048576.0) + "MB.  mem_cache: " + str(mem_cache / 1048576.0) +
+           "MB.  total: " + str(total) + "\n")
+    print(msg)
+    if logger:
+        logger.write(msg)
 
 
 def get_fullname_of_model(abbr):
@@ -256,6 +275,8 @@ def main(argv=None):
     train_len = len(db)
     max_iter = args.maxEpoches * train_len
     step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph) and not sbm)
+    mem = (lambda prefix: log_mem(logger, prefix)) if (args.log_mem and is0) else (lambda prefix: None)
+    step.mem_hook = mem
     say("=====> Begin to train: %d iterations per epoch, %d epochs, %d GPU(s) x %d pairs" % (
         train_len, args.maxEpoches, world, per_rank))
     t_start = time.time()
@@ -267,12 +288,14 @@ def main(argv=None):
         else:
             db.next_batch()
         for i_iter in range(train_len):
+            mem(" Start batch")
             batch = db[i_iter]
             lr = lr_poly(args.learning_rate, i_iter + epoch * train_len, max_iter, args.power, epoch)
             lrs = [0.01 * lr, 10 * lr]  # train.py:171-172
             ins = (batch["target"].to(dev), batch["search_0"].to(dev), batch["target_depth"].to(dev),
                    batch["search_0_depth"].to(dev), batch["target_gt"].unsqueeze(1).to(dev).float(),
                    batch["search_0_gt"].unsqueeze(1).to(dev).float())
+            mem(" After feeding data to GPU")
             if sbm:
                 loss = step.run_batch(*ins, lrs)
             elif not captured:
@@ -284,13 +307,24 @@ def main(argv=None):
             else:
                 step.load(*ins)
                 loss = step(lrs)
-            lv = float(loss.item())
+            if world > 1:
+                # the reference's loss is computed on outputs gathered from the whole global
+                # batch: with equal shards (and the global BCE weight) that is the rank mean
+                lt = loss.detach().clone()
+                dist.all_reduce(lt)
+                lv = float(lt.item()) / world
+            else:
+                lv = float(loss.item())
             loss_history.append(lv)
             say("===> Epoch[{}]({}/{}): Loss: {:.10f}  lr: {:.5f}".format(epoch, i_iter, train_len, lv, lr))
             if logger:
                 logger.write("Epoch[{}]({}/{}):     Loss: {:.10f}      lr: {:.5f}\n".format(
                     epoch, i_iter, train_len, lv, lr))
                 logger.flush()
+            del batch, ins
+            gc.collect()
+            torch.cuda.empty_cache()
+            mem(" After GC")
         step.sync_buffers()  # rank 0's BN buffers, like DataParallel's replica 0
         if is0:
             path = os.path.join(args.snapshot_dir, "snapshot_%s_%d.pth" % (args.dataset, epoch))
