@@ -29,6 +29,13 @@ _SIGS = {
     "cn_conv_wgrad_workspace_floats": (_S, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "cn_conv_wgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cn_splitk_reduce": (_I, [_P, _I, _L, _L, _P, _I, _P]),
+    "cn_conv_fwd_bn_workspace_floats": (_S, [_I, _I, _I, _I]),
+    "cn_conv_fwd_bn": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I,
+                            _I, _P, _P, _P, _P, _P, _F, _F, _P]),
+    "cn_conv_dgrad_bn_workspace_floats": (_S, [_I, _I, _I, _I]),
+    "cn_conv_dgrad_bn": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _L, _I, _I, _P,
+                              _L, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "cn_bn_bwd_apply": (_I, [_I, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _P, _P, _P, _L, _P]),
     "cn_gemm": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _I, _I, _F, _P, _I, _I, _L, _P]),
     "cn_bn_workspace_floats": (_S, [_I, _I, _I, _I]),
     "cn_bn_stats": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P]),

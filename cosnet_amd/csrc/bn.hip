@@ -215,6 +215,77 @@ __global__ __launch_bounds__(256) void bn_stats_finalize(const float* __restrict
   if (run_mean) { run_mean[c] = (float)rm; run_var[c] = (float)rv; }
 }
 
+// ---- forward statistics from the conv epilogue (gemm.h st_mode 1) ---------------------------
+// Per M-tile t and column c the GEMM wrote K (the tile's first row), and shifted sums
+// [sum(c-K), sum((c-K)^2)] of the rows in the tile's first segment and of the rows in the next.
+// Each tile's sums are turned into plain sum / sum of squares in double and added over the tiles
+// in a fixed order (lanes stride the tiles, then a shuffle tree and the 4 waves in order):
+// deterministic, and double keeps the final var = E[x^2] - mean^2 exact enough for any data
+// whose per-tile spread fp32 resolves.
+template <int NSEG>
+__global__ __launch_bounds__(256) void bn_tile_stats_finalize(const float* __restrict__ ws, long long plane,
+                                                              int mtiles, int BM, int M, int seg_rows,
+                                                              int C, float* mean, float* invstd,
+                                                              float* run_mean, float* run_var,
+                                                              float momentum, float eps) {
+  const int c0 = blockIdx.x * FCH;
+  const int ch = threadIdx.x % FCH, lane = threadIdx.x / FCH, c = c0 + ch;
+  double d1[NSEG], d2[NSEG];
+#pragma unroll
+  for (int s = 0; s < NSEG; ++s) { d1[s] = 0.0; d2[s] = 0.0; }
+  if (c < C) {
+    for (int t = lane; t < mtiles; t += 256 / FCH) {
+      const int r0 = t * BM, r1 = min(M, r0 + BM);
+      const int sA = r0 / seg_rows;
+      const int endA = min(r1, (sA + 1) * seg_rows);
+      const double nA = endA - r0, nB = r1 - endA;
+      const long long o = (long long)t * C + c;
+      const double K = ws[o];
+      const double a1 = ws[o + plane], a2 = ws[o + 2 * plane];
+#pragma unroll
+      for (int s = 0; s < NSEG; ++s) {
+        if (s == sA) { d1[s] += nA * K + a1; d2[s] += a2 + 2.0 * K * a1 + nA * K * K; }
+        if (s == sA + 1 && nB > 0) {
+          const double b1 = ws[o + 3 * plane], b2 = ws[o + 4 * plane];
+          d1[s] += nB * K + b1;
+          d2[s] += b2 + 2.0 * K * b1 + nB * K * K;
+        }
+      }
+    }
+  }
+  __shared__ double red[2 * NSEG][4][FCH];
+  const int wave = threadIdx.x / 64;
+#pragma unroll
+  for (int s = 0; s < NSEG; ++s) {
+#pragma unroll
+    for (int o = FCH; o < 64; o <<= 1) {
+      d1[s] += __shfl_xor(d1[s], o, 64);
+      d2[s] += __shfl_xor(d2[s], o, 64);
+    }
+    if ((threadIdx.x & 63) < FCH) { red[2 * s][wave][ch] = d1[s]; red[2 * s + 1][wave][ch] = d2[s]; }
+  }
+  __syncthreads();
+  if (threadIdx.x >= FCH || c >= C) return;
+  double rm = 0, rv = 0;
+  if (run_mean) { rm = run_mean[c]; rv = run_var[c]; }
+  const double n = seg_rows;
+  for (int s = 0; s < NSEG; ++s) {
+    const double s1 = ((red[2 * s][0][ch] + red[2 * s][1][ch]) + red[2 * s][2][ch]) + red[2 * s][3][ch];
+    const double s2 = ((red[2 * s + 1][0][ch] + red[2 * s + 1][1][ch]) + red[2 * s + 1][2][ch]) + red[2 * s + 1][3][ch];
+    const double md = s1 / n;
+    double var = s2 / n - md * md;
+    if (var < 0) var = 0;
+    mean[s * C + c] = (float)md;
+    invstd[s * C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (run_mean) {
+      const double unb = n > 1 ? var * n / (n - 1) : var;
+      rm = (float)((1.0 - momentum) * rm + momentum * md);
+      rv = (float)((1.0 - momentum) * rv + momentum * unb);
+    }
+  }
+  if (run_mean) { run_mean[c] = (float)rm; run_var[c] = (float)rv; }
+}
+
 __global__ void bn_eval_params(const float* rm, const float* rv, int C, float eps, float* mean, float* invstd) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -523,6 +594,65 @@ extern "C" int cn_bn_stats(int dtype, const void* x, long long ldx, int P, int n
                                  momentum, eps, ws, st);
   return bn_stats_launch<float>((const float*)x, ldx, P, nseg, C, mean, invstd, run_mean, run_var,
                                 momentum, eps, ws, st);
+}
+
+int cn_bn_tile_stats_impl(const float* ws, long long plane, int mtiles, int BM, int M, int nseg, int C,
+                          float* mean, float* invstd, float* run_mean, float* run_var, float momentum,
+                          float eps, hipStream_t st) {
+  if (nseg < 1 || M % nseg) return CN_ERR_SHAPE;
+  const int seg_rows = M / nseg;
+  const dim3 fin((C + FCH - 1) / FCH);
+#define CN_TF(NS)                                                                                    \
+  hipLaunchKernelGGL((bn_tile_stats_finalize<NS>), fin, dim3(256), 0, st, ws, plane, mtiles, BM, M, \
+                     seg_rows, C, mean, invstd, run_mean, run_var, momentum, eps)
+  switch (nseg) {
+    case 1: CN_TF(1); break;
+    case 2: CN_TF(2); break;
+    default: return CN_ERR_UNSUPPORTED;
+  }
+#undef CN_TF
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+// Backward sums from the dgrad epilogue (gemm.h st_mode 2): planes [sum dz, sum dz*xh] per
+// M-tile -> sum_dz[c], sum_dzxh[c] (bn_bwd_finalize over S = mtiles splits, same layout).
+int cn_bn_tile_bwd_impl(const float* ws, int mtiles, int C, float* sum_dz, float* sum_dzxh,
+                        hipStream_t st) {
+  const dim3 fin((C + FCH - 1) / FCH);
+  hipLaunchKernelGGL(bn_bwd_finalize<2>, fin, dim3(256), 0, st, ws, mtiles, C, sum_dz, sum_dzxh,
+                     (float*)nullptr);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cn_bn_bwd_apply(int dtype, const void* x, long long ldx, const void* dy, long long lddy,
+                               int P, int C, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, const float* sum_dz,
+                               const float* sum_dzxh, void* dx, long long lddx, hipStream_t st) {
+  const int vec = dtype == DT_BF16 ? 8 : 4;
+  if (C % vec || ldx % vec || lddy % vec || lddx % vec) return CN_ERR_ALIGN;
+  if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
+      !aligned16(sum_dz) || !aligned16(sum_dzxh))
+    return CN_ERR_ALIGN;
+  if (P < 1) return CN_ERR_SHAPE;
+  int gx, gy;
+  // act 3: ReLU mask recomputed from x with the forward's affine (no residual on these BNs)
+  if (dtype == DT_BF16) {
+    gy = grid_rows<bf16>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
+    hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
+                       (const bf16*)dy, lddy, (const bf16*)nullptr, 0ll, P, C, mean, invstd, gamma,
+                       beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (bf16*)dx, lddx,
+                       (bf16*)nullptr, 0ll);
+  } else {
+    gy = grid_rows<float>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
+    hipLaunchKernelGGL(bn_bwd_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
+                       (const float*)dy, lddy, (const float*)nullptr, 0ll, P, C, mean, invstd, gamma,
+                       beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (float*)dx, lddx,
+                       (float*)nullptr, 0ll);
+  }
+  CN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int cn_bn_eval_params(const float* run_mean, const float* run_var, int C, float eps,

@@ -58,6 +58,109 @@ extern "C" int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H
   return cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
 }
 
+// ---- conv + BatchNorm epilogues ------------------------------------------------------------
+int cn_bn_tile_stats_impl(const float* ws, long long plane, int mtiles, int BM, int M, int nseg, int C,
+                          float* mean, float* invstd, float* run_mean, float* run_var, float momentum,
+                          float eps, hipStream_t st);
+int cn_bn_tile_bwd_impl(const float* ws, int mtiles, int C, float* sum_dz, float* sum_dzxh,
+                        hipStream_t st);
+
+static int conv_fwd_args(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                         const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                         const float* bias, void* y, long long ldy, int OH, int OW, GemmArgs& a,
+                         int& la) {
+  if (Cin % vec_of(dtype) || ldx % vec_of(dtype)) return CN_ERR_ALIGN;
+  if (OH != (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  if (OW != (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  a = gemm_defaults();
+  a.M = N * OH * OW; a.N = Cout; a.K = KH * KW * Cin;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = x; a.lda = ldx;
+  a.B = w; a.ldb = a.K;
+  a.C = y; a.ldc = ldy;
+  a.bias = bias;
+  la = L_KC_CONV;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) la = L_KC_DENSE;
+  else a.ga = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  return 0;
+}
+
+static long long mtiles_of(int dtype, int M, int N, int K) {
+  const int bm = cn_gemm_bm(dtype, M, N, K, -1);
+  return (M + bm - 1) / bm;
+}
+
+extern "C" size_t cn_conv_fwd_bn_workspace_floats(int dtype, int M, int Cout, int K) {
+  return (size_t)5 * mtiles_of(dtype, M, Cout, K) * Cout;
+}
+
+// y = conv2d(x, w) + bias, and the train-mode BatchNorm statistics of y computed in the GEMM
+// epilogue (no separate pass over y): mean / invstd [nseg][Cout] of each of the nseg stacked
+// row segments (frames), running stats updated segment after segment.
+extern "C" int cn_conv_fwd_bn(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                              const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                              const float* bias, void* y, long long ldy, int OH, int OW, int nseg,
+                              float* ws, float* mean, float* invstd, float* run_mean, float* run_var,
+                              float momentum, float eps, hipStream_t st) {
+  GemmArgs a;
+  int la;
+  int rc = conv_fwd_args(dtype, x, ldx, N, H, W, Cin, w, Cout, KH, KW, stride, pad, dil, bias, y,
+                         ldy, OH, OW, a, la);
+  if (rc) return rc;
+  if (nseg < 1 || a.M % nseg || !ws) return CN_ERR_SHAPE;
+  const int bm = cn_gemm_bm(dtype, a.M, a.N, a.K, -1);
+  const long long mt = (a.M + bm - 1) / bm;
+  a.st_mode = 1;
+  a.st_ws = ws;
+  a.st_plane = mt * Cout;
+  a.st_seg_rows = a.M / nseg;
+  rc = cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
+  if (rc) return rc;
+  return cn_bn_tile_stats_impl(ws, a.st_plane, (int)mt, bm, a.M, nseg, Cout, mean, invstd, run_mean,
+                               run_var, momentum, eps, st);
+}
+
+extern "C" size_t cn_conv_dgrad_bn_workspace_floats(int dtype, int M, int Cin, int K) {
+  return (size_t)2 * mtiles_of(dtype, M, Cin, K) * Cin;
+}
+
+// dy = conv2d input-gradient (stride 1) AND, in the GEMM epilogue, the reduction of the backward
+// of the BatchNorm + ReLU that produced the conv's input: with x the BN's pre-activation input
+// (same [P][Cin] rows), dz = dy * (relu mask recomputed from x with the forward affine),
+// sum_dz[c] = sum dz, sum_dzxh[c] = sum dz * (x - mean) * invstd  (= the BN's dbeta / dgamma).
+// cn_bn_bwd_apply then forms dx of the BN from these sums.
+extern "C" int cn_conv_dgrad_bn(int dtype, const void* dy, long long lddy, int N, int OH, int OW,
+                                int Cout, const void* wt, int Cin, int KH, int KW, int pad, int dil,
+                                void* dx, long long lddx, int H, int W, const void* x, long long ldx,
+                                const float* mean, const float* invstd, const float* gamma,
+                                const float* beta, float* sum_dz, float* sum_dzxh, float* ws,
+                                hipStream_t st) {
+  if (Cout % vec_of(dtype) || lddy % vec_of(dtype) || ldx % vec_of(dtype)) return CN_ERR_ALIGN;
+  if (!ws || !x || !mean || !invstd) return CN_ERR_SHAPE;
+  GemmArgs a = gemm_defaults();
+  a.N = Cin; a.K = KH * KW * Cout;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = dy; a.lda = lddy;
+  a.B = wt; a.ldb = a.K;
+  a.C = dx; a.ldc = lddx;
+  a.M = N * H * W;
+  int la = L_KC_DENSE;
+  if (!(KH == 1 && KW == 1 && pad == 0)) {
+    la = L_KC_CONV;
+    a.ga = make_geom(N, OH, OW, Cout, H, W, KH, KW, 1, pad, pad, -dil, -dil);
+  }
+  const int bm = cn_gemm_bm(dtype, a.M, a.N, a.K, -1);
+  const long long mt = (a.M + bm - 1) / bm;
+  a.st_mode = 2;
+  a.st_ws = ws;
+  a.st_plane = mt * Cin;
+  a.br_x = x; a.br_ldx = ldx;
+  a.br_mean = mean; a.br_invstd = invstd; a.br_gamma = gamma; a.br_beta = beta;
+  int rc = cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
+  if (rc) return rc;
+  return cn_bn_tile_bwd_impl(ws, (int)mt, Cin, sum_dz, sum_dzxh, st);
+}
+
 extern "C" int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, int OH, int OW,
                              int Cout, const void* wt, int Cin, int KH, int KW, int stride,
                              int pad, int dil, void* dx, long long lddx, int H, int W,

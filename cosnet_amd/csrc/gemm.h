@@ -36,11 +36,28 @@ struct GemmArgs {
   long long slab;              // elements between split-K slabs (c_mode 3)
   float alpha;
   int cfg;                     // tile configuration (gemm.hip kCfg), -1 = shape heuristic
+  // BatchNorm epilogues (batch == 1, nsplit == 1, row_map == 0, c_mode 0 only):
+  //  st_mode 1: per-(M-tile, column) statistics of the STORED C for train-mode BN: planes
+  //             [K, sum(c-K), sum((c-K)^2)] for the tile's first segment (rows < the next
+  //             multiple of st_seg_rows) and [sum, sumsq] for the second, K = the tile's first
+  //             row (a per-tile shift); plane stride st_plane floats, row = M-tile, col = n.
+  //  st_mode 2: BN backward reduce of the stored C (= dy of a BN + ReLU whose pre-BN input is
+  //             br_x): dz = dy * (br_x * k1 + sf > 0), xh = (br_x - mu) * is;
+  //             planes [sum dz, sum dz * xh].  k1 = gamma * is, sf = beta - mu * k1.
+  int st_mode;
+  float* st_ws;
+  long long st_plane;
+  int st_seg_rows;
+  const void* br_x; long long br_ldx;
+  const float* br_mean; const float* br_invstd; const float* br_gamma; const float* br_beta;
 };
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);
 // Tile configuration the dispatcher picks for a bf16 problem, and its block count.
 int cn_gemm_pick(int M, int N, int K, int batch_splits);
 long long cn_gemm_cfg_blocks(int cfg, int M, int N);
+// Tile rows (BM) of the configuration cn_gemm_dispatch uses for a problem (BN epilogues size
+// their per-M-tile partials with it).
+int cn_gemm_bm(int dtype, int M, int N, int K, int cfg_or_minus1);
 int cn_splitk_reduce_impl(const float* ws, int nsplit, long long slab, long long n, float* out,
                           int accumulate, hipStream_t st);

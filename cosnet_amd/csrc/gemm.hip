@@ -18,6 +18,7 @@
 // K step = 128 bytes of k (64 bf16 / 32 fp32); register-staged double-buffered LDS.
 #include "common.h"
 #include "gemm.h"
+#include "../../include/cosnet_hip.h"
 
 #include <type_traits>
 
@@ -282,8 +283,11 @@ __device__ __forceinline__ void raw_barrier() {
 #define CN_GEMM_PRIO 0
 #endif
 
-template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
+// BN-epilogue variants of the 128-row tiles keep <= 128 VGPRs (4 waves per SIMD = two 512-thread
+// blocks per CU, the
+// occupancy the plain kernel has from its LDS footprint; HIP's 2nd bound is waves per SIMD).
+template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0>
+__global__ __launch_bounds__(WM * WN * 64, (EPI && BM * BN <= 128 * 128) ? 4 : 1) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
   constexpr int VEC = VecOf<T>::N;
   constexpr int BK = 8 * VEC;
@@ -470,6 +474,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
   // Epilogue: stage alpha*acc (fp32) through LDS, HR tile rows per pass, as [HR][BN+4]; then
   // every thread writes 8 consecutive columns of a row (16-B bf16 / 2x16-B fp32 stores, or 8
   // contiguous atomics).  Lane holds C[4g + r][l & 15] of each 16x16 block.
+  // BN epilogues (st_mode, gemm.h) accumulate per-column partials of the stored values in the
+  // same loop (registers), reduced over the block in a fixed order at the end.
   constexpr int LDC = BN + 4;
   constexpr int HR = (BM * LDC * 4 <= S * STAGE) ? BM
                    : ((BM / 2) * LDC * 4 <= S * STAGE) ? BM / 2
@@ -480,8 +486,48 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
   constexpr int GPR = BN / 8;            // 8-column groups per row
   constexpr int RPP = NT / GPR;          // rows per pass
+  constexpr int smode = EPI;             // BN epilogue (compile-time: its registers would
+                                         // otherwise cost every plain GEMM occupancy)
+  const int c0t = (tid % GPR) * 8;       // this thread's columns within the tile (fixed)
+  float sk[8], sa1[8], sa2[8], sb1[8], sb2[8];
+  float bk1[8], bsf[8], bmu[8], bis[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sk[e] = 0.f; sa1[e] = sa2[e] = sb1[e] = sb2[e] = 0.f; }
+  int segA_end = 0x7fffffff;
+  if constexpr (smode == 1) {
+    segA_end = (m0 / p.st_seg_rows + 1) * p.st_seg_rows;
+  } else if constexpr (smode == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n0 + c0t + e;
+      const bool in = c < p.N;
+      const float g = in ? (p.br_gamma ? p.br_gamma[c] : 1.f) : 0.f;
+      const float b = in ? (p.br_beta ? p.br_beta[c] : 0.f) : 0.f;
+      bmu[e] = in ? p.br_mean[c] : 0.f;
+      bis[e] = in ? p.br_invstd[c] : 0.f;
+      bk1[e] = g * bis[e];              // the forward apply's affine (bn.hip bn_apply_k): the
+      bsf[e] = b - bmu[e] * bk1[e];     // recomputed ReLU mask has exactly the forward's sign
+    }
+  }
+  constexpr int IT = HR / RPP;          // rows per thread per pass
+  static_assert(IT * RPP == HR, "epilogue rows per pass must be a multiple of the row stride");
 #pragma unroll 1
   for (int pass = 0; pass < BM / HR; ++pass) {
+    u32x4 xpf[smode == 2 ? IT * (int)sizeof(CT) / 2 : 1];
+    if constexpr (smode == 2) {
+      // BN-backward epilogue: issue this pass's loads of the pre-BN input first, so they are in
+      // flight while the accumulators are staged through LDS
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int row = m0 + pass * HR + tid / GPR + it * RPP;
+        const int col = n0 + c0t;
+        constexpr int Q = (int)sizeof(CT) / 2;  // 16-B chunks per 8 elements
+        const bool ok = row < p.M && col + 8 <= p.N;
+        const u32x4* src = (const u32x4*)((const CT*)p.br_x + (long long)(ok ? row : m0) * p.br_ldx + (ok ? col : 0));
+#pragma unroll
+        for (int q = 0; q < Q; ++q) xpf[it * Q + q] = src[q];
+      }
+    }
     {
       const int g = lane >> 4;
 #pragma unroll
@@ -496,8 +542,16 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
       }
     }
     __syncthreads();
-#pragma unroll 1
-    for (int rr = tid / GPR; rr < HR; rr += RPP) {
+    if (smode == 1 && pass == 0) {  // per-tile shift: the tile's first row (with bias)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = n0 + c0t + e;
+        sk[e] = cs[c0t + e] + ((p.bias && c < p.N) ? p.bias[c] : 0.f);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int rr = tid / GPR + it * RPP;
       const int row = m0 + pass * HR + rr;
       if (row >= p.M) continue;
       long long drow = row;
@@ -507,7 +561,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
         fdivmod(rem, p.rm_div_OW, oy, ox);
         drow = ((long long)im * p.rm_H + 2 * oy) * p.rm_W + 2 * ox;
       }
-      const int c0 = (tid % GPR) * 8;
+      const int c0 = c0t;
       const int col = n0 + c0;
       if (col >= p.N) continue;
       float v[8];
@@ -531,7 +585,9 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += q[e];
           }
-          *(u32x4*)dst = Chunk<bf16>::pack(v);
+          const u32x4 pk = Chunk<bf16>::pack(v);
+          *(u32x4*)dst = pk;
+          if (smode) Chunk<bf16>::unpack(pk, v);  // statistics of the values as stored
         } else {
           if (cmode == 2) {
             f32x4 q0 = *(const f32x4*)dst, q1 = *(const f32x4*)(dst + 4);
@@ -544,10 +600,87 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(GemmArgs p) {
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (col + e < p.N) store_c<CT>(dst + e, v[e], cmode);
+          if (col + e < p.N) {
+            store_c<CT>(dst + e, v[e], cmode);
+            v[e] = tof((CT)v[e]);
+          }
+      }
+#ifndef CN_EPI_NOACC
+      if constexpr (smode == 1) {
+        const bool inA = row < segA_end;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (col + e < p.N) ? v[e] - sk[e] : 0.f;
+          if (inA) { sa1[e] += d; sa2[e] = fmaf(d, d, sa2[e]); }
+          else { sb1[e] += d; sb2[e] = fmaf(d, d, sb2[e]); }
+        }
+      } else if constexpr (smode == 2) {
+        float xv[8];
+        if (full) {
+          if constexpr (sizeof(CT) == 2) Chunk<bf16>::unpack(xpf[it], xv);
+          else { *(u32x4*)&xv[0] = xpf[2 * it]; *(u32x4*)&xv[4] = xpf[2 * it + 1]; }
+        } else {
+          const CT* xs = (const CT*)p.br_x + (long long)row * p.br_ldx + col;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xv[e] = (col + e < p.N) ? tof(xs[e]) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float dd = (col + e < p.N && fmaf(xv[e], bk1[e], bsf[e]) > 0.f) ? v[e] : 0.f;
+          const float xh = (xv[e] - bmu[e]) * bis[e];
+          sa1[e] += dd;
+          sa2[e] = fmaf(dd, xh, sa2[e]);
+        }
+      }
+#endif
+    }
+    __syncthreads();
+  }
+#ifdef CN_EPI_NORED
+  if constexpr (false) {
+#else
+  if constexpr (smode != 0) {
+#endif
+    // Column partials: lanes sharing this thread's column group (lane ^ GPR, ^2 GPR, ...) by
+    // shuffles, then the waves in order through LDS; one row of each plane per M-tile.
+    constexpr int NW = NT / 64;
+    const int nq = smode == 1 ? 4 : 2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = GPR; o < 64; o <<= 1) {
+        sa1[e] += __shfl_xor(sa1[e], o, 64);
+        sa2[e] += __shfl_xor(sa2[e], o, 64);
+        if (smode == 1) {
+          sb1[e] += __shfl_xor(sb1[e], o, 64);
+          sb2[e] += __shfl_xor(sb2[e], o, 64);
+        }
+      }
+    }
+    float* red = cs;  // [NW][4][BN]
+    if (lane < GPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 4 + 0) * BN + c0t + e] = sa1[e];
+        red[(wave * 4 + 1) * BN + c0t + e] = sa2[e];
+        red[(wave * 4 + 2) * BN + c0t + e] = sb1[e];
+        red[(wave * 4 + 3) * BN + c0t + e] = sb2[e];
       }
     }
     __syncthreads();
+    float* ws = p.st_ws + (long long)tm * p.N;
+    for (int t = tid; t < nq * BN; t += NT) {
+      const int q = t / BN, c = t % BN;
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) a += red[(w * 4 + q) * BN + c];
+      if (n0 + c < p.N) ws[(long long)(smode == 1 ? q + 1 : q) * p.st_plane + n0 + c] = a;
+    }
+    if (smode == 1 && tid < GPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n0 + c0t + e < p.N) ws[n0 + c0t + e] = sk[e];
+    }
   }
 }
 
@@ -601,14 +734,31 @@ static int pick_cfg(const GemmArgs& a, int batch) {
   return heuristic_cfg(a.M, a.N, a.K, batch * a.nsplit);
 }
 
-template <class T, class CT, int C, int LA, int LB>
+template <class T, class CT, int C, int LA, int LB, int EPI = 0>
 static int launch_c(const GemmArgs& a, int batch, hipStream_t st) {
   constexpr TileCfg c = kCfg[C];
   dim3 grid((a.M + c.bm - 1) / c.bm, (a.N + c.bn - 1) / c.bn, batch * a.nsplit);
-  hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB>), grid,
+  hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB, EPI>), grid,
                      dim3(c.wm * c.wn * 64), 0, st, a);
   CN_CHECK_LAUNCH();
   return 0;
+}
+
+// BN-epilogue GEMMs (conv fwd with statistics, stride-1 dgrad with the BN backward reduce):
+// only the tiles the shape heuristic picks for conv fwd / dgrad are instantiated.
+template <class T, int LA, int EPI>
+static int launch_epi(const GemmArgs& a, hipStream_t st) {
+  if constexpr (sizeof(T) == 4) {
+    if (a.N <= 64 || cfg_blocks(1, a, 1) < 384) return launch_c<T, T, 0, LA, L_KC_DENSE, EPI>(a, 1, st);
+    return launch_c<T, T, 1, LA, L_KC_DENSE, EPI>(a, 1, st);
+  } else {
+    switch (pick_cfg(a, 1)) {
+      case 10: return launch_c<T, T, 10, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 11: return launch_c<T, T, 11, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 12: return launch_c<T, T, 12, LA, L_KC_DENSE, EPI>(a, 1, st);
+      default: return CN_ERR_UNSUPPORTED;
+    }
+  }
 }
 
 template <class T, class CT, int LA, int LB>
@@ -655,6 +805,19 @@ static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
+  if (a.st_mode) {
+    if (batch != 1 || a.nsplit != 1 || a.row_map || a.c_mode ||
+        lb != L_KC_DENSE || (la != L_KC_DENSE && la != L_KC_CONV))
+      return CN_ERR_UNSUPPORTED;
+#define CN_EPI(T_, M_) \
+    return la == L_KC_DENSE ? launch_epi<T_, L_KC_DENSE, M_>(a, st) : launch_epi<T_, L_KC_CONV, M_>(a, st)
+    if (dtype == DT_BF16) {
+      if (a.st_mode == 1) CN_EPI(bf16, 1); else CN_EPI(bf16, 2);
+    } else {
+      if (a.st_mode == 1) CN_EPI(float, 1); else CN_EPI(float, 2);
+    }
+#undef CN_EPI
+  }
   if (dtype == DT_BF16) {
     return c_f32 ? launch_kinds<bf16, float>(a, la, lb, batch, st)
                  : launch_kinds<bf16, bf16>(a, la, lb, batch, st);
@@ -662,6 +825,13 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     return launch_kinds<float, float>(a, la, lb, batch, st);
   }
   return -11;
+}
+
+int cn_gemm_bm(int dtype, int M, int N, int K, int cfg) {
+  if (dtype != DT_BF16) return kCfg[1].bm;  // the fp32 path: configs 0 / 1 (both 128 rows)
+  if (g_force_cfg >= 0 && g_force_cfg < kNumCfg) return kCfg[g_force_cfg].bm;
+  if (cfg >= 0 && cfg < kNumCfg) return kCfg[cfg].bm;
+  return kCfg[heuristic_cfg(M, N, K, 1)].bm;
 }
 
 int cn_gemm_pick(int M, int N, int K, int batch_splits) {

@@ -42,6 +42,30 @@ def seg_stats(x, bn, training, nseg):
     return SegStats(bn_stats(x, bn, training, nseg=nseg), nseg, x.shape[1])
 
 
+def fuse_stats(cout, kdim):
+    """The BN-statistics epilogue pays off on long-K, narrow convs (measured per shape,
+    tools/epi_probe.py: layer-3 1x1 1024->256 34 vs 40 us, 3x3 52 vs 56 us, ASPP 446 vs 480 us);
+    on short-K / wide outputs (256->1024 1x1: 61 vs 51 us) the separate pass is cheaper."""
+    return kdim >= 1024 and cout <= 512
+
+
+def fuse_bwd(cin, kdim):
+    """Same for the dgrad epilogue that reduces the BN backward (43 vs 45 us on the layer-3 3x3,
+    30 vs 34 us on the 256->1024 1x1; a loss on 1024-wide outputs)."""
+    return kdim >= 1024 and cin <= 256
+
+
+def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=None):
+    """conv -> raw output c and the BN statistics of c per segment.  Train mode: the statistics
+    come out of the conv's GEMM epilogue where that is cheaper (ops.conv_fwd_bn, no pass over c),
+    else a separate statistics pass; eval: running statistics."""
+    if training and fuse_stats(cout, wf.shape[1]):
+        c, oh, ow, st = ops.conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg, bias=bias)
+        return c, oh, ow, SegStats(st, nseg, cout)
+    c, oh, ow = conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=bias)
+    return c, oh, ow, seg_stats(c, bn, training, nseg)
+
+
 def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
     return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
                     rstats=None if rstats is None else (rstats.mean, rstats.invstd), rbn=rbn,
@@ -57,8 +81,7 @@ def stem_fwd(res, imgs, nseg, dt, rec):
         nv.call("cn_nchw_to_nhwc", nv.dtype_code(dt), img.data_ptr(), n1, cimg, h, w, 8,
                 x[i * n1 * h * w:].data_ptr(), nv.stream())
     wf, _ = WCACHE.get(res.conv1.weight, dt, cin_pad=8, need_t=False)
-    c, oh, ow = conv_fwd(x, n, h, w, wf, 64, 7, 2, 3, 1)
-    st = seg_stats(c, res.bn1, res.training, nseg)
+    c, oh, ow, st = conv_bn(x, n, h, w, wf, 64, 7, 2, 3, 1, res.bn1, res.training, nseg)
     y = seg_apply(c, st, res.bn1, act=1)
     ph, pw = ops.pool_out(oh), ops.pool_out(ow)
     out = torch.empty((n * ph * pw, 64), dtype=dt, device=x.device)
@@ -83,6 +106,17 @@ def stem_bwd(item, dout, grads):
     grads[res.bn1.bias] = db
 
 
+def dgrad_bn_bwd(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn):
+    """Stride-1 conv dgrad followed by the backward of the BN + ReLU (mask from x) that fed the
+    conv: returns (dx of the BN input, dgamma, dbeta)."""
+    if fuse_bwd(cin, wt.shape[1]):
+        dyb, dg, db = ops.conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn)
+        return ops.bn_bwd_apply(x, dyb, stats, bn, dg, db), dg, db
+    dyb = conv_dgrad(dy, n, oh, ow, wt, cin, k, 1, pad, dil, oh, ow)
+    dx, dg, db, _ = bn_bwd(x, dyb, None, stats, bn, act=1)
+    return dx, dg, db
+
+
 # ---- bottleneck ----------------------------------------------------------------------------------
 def bottleneck_fwd(blk, x, geo, nseg, rec):
     n, h, w = geo
@@ -93,20 +127,16 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     w1f, w1t = WCACHE.get(blk.conv1.weight, dt)
     w2f, w2t = WCACHE.get(blk.conv2.weight, dt)
     w3f, w3t = WCACHE.get(blk.conv3.weight, dt)
-    c1, oh, ow = conv_fwd(x, n, h, w, w1f, planes, 1, s, 0, 1)
-    st1 = seg_stats(c1, blk.bn1, tr, nseg)
+    c1, oh, ow, st1 = conv_bn(x, n, h, w, w1f, planes, 1, s, 0, 1, blk.bn1, tr, nseg)
     y1 = seg_apply(c1, st1, blk.bn1, act=1)
-    c2, _, _ = conv_fwd(y1, n, oh, ow, w2f, planes, 3, 1, d, d)
-    st2 = seg_stats(c2, blk.bn2, tr, nseg)
+    c2, _, _, st2 = conv_bn(y1, n, oh, ow, w2f, planes, 3, 1, d, d, blk.bn2, tr, nseg)
     y2 = seg_apply(c2, st2, blk.bn2, act=1)
-    c3, _, _ = conv_fwd(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1)
-    st3 = seg_stats(c3, blk.bn3, tr, nseg)
+    c3, _, _, st3 = conv_bn(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1, blk.bn3, tr, nseg)
     cd = std = wdt = None
     if blk.downsample is not None:
         wdf, wdt = WCACHE.get(blk.downsample[0].weight, dt)
         bnd = blk.downsample[1]
-        cd, _, _ = conv_fwd(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1)
-        std = seg_stats(cd, bnd, tr, nseg)
+        cd, _, _, std = conv_bn(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1, bnd, tr, nseg)
         y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd)
     else:
         y = seg_apply(c3, st3, blk.bn3, act=1, res=x)
@@ -131,11 +161,11 @@ def bottleneck_bwd(item, dy, grads, need_dx=True):
         dx = torch.empty_like(x)
         dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx)
     dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
-    dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
-    dc2, dg2, db2, _ = bn_bwd(c2, dy2, None, st2[0], blk.bn2, act=1)
+    # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where
+    # that is cheaper (fuse_bwd)
+    dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2)
     dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
-    dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
-    dc1, dg1, db1, _ = bn_bwd(c1, dy1, None, st1[0], blk.bn1, act=1)
+    dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1)
     dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
     if need_dx:
         dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
@@ -165,8 +195,7 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     pool = torch.empty((n, 2048), dtype=dt, device=dev)
     ops.avgpool(x, n, hw, 1.0 / hw, pool)
     wcf, wct = WCACHE.get(mod.conv.weight, dt)
-    cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=mod.conv.bias)
-    stp = seg_stats(cp, mod.bn_x, tr, nseg)
+    cp, _, _, stp = conv_bn(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, mod.bn_x, tr, nseg, bias=mod.conv.bias)
     yp = seg_apply(cp, stp, mod.bn_x, act=1)
     nv.call("cn_bcast_rows", ops.dtc(yp), yp.data_ptr(), n, hw, 512, 1.0, cat.data_ptr(), 2560, 0,
             nv.stream())
@@ -176,15 +205,13 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     cs, sts, wts = [], [], []
     for bi, (cm, bnm, k, dd) in enumerate(convs):
         wf, wt = WCACHE.get(cm.weight, dt)
-        ci, _, _ = conv_fwd(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bias=cm.bias)
-        st = seg_stats(ci, bnm, tr, nseg)
+        ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias)
         seg_apply(ci, st, bnm, act=1, out=cat[:, 512 * (bi + 1):512 * (bi + 2)])
         cs.append(ci)
         sts.append(st)
         wts.append(wt)
     wbf, wbt = WCACHE.get(mod.bottleneck.weight, dt)
-    cb, _, _ = conv_fwd(cat, n, h, w, wbf, 256, 3, 1, 1, 1, bias=mod.bottleneck.bias)
-    stb = seg_stats(cb, mod.bn, tr, nseg)
+    cb, _, _, stb = conv_bn(cat, n, h, w, wbf, 256, 3, 1, 1, 1, mod.bn, tr, nseg, bias=mod.bottleneck.bias)
     out = seg_apply(cb, stb, mod.bn, act=2, prelu=mod.prelu.weight)
     if rec is not None:
         rec.append(("aspp", mod, (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out),

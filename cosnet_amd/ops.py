@@ -182,6 +182,70 @@ def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
     return out, oh, ow
 
 
+def conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg=1, bias=None):
+    """Train mode: y = conv(x) (+ bias) and the BN batch statistics of y from the GEMM epilogue
+    (cn_conv_fwd_bn: no pass of its own over y).  Returns (y, oh, ow, (mean, invstd)) with
+    [nseg*cout] statistics; bn.running_* updated once per segment like bn_stats."""
+    cin = wf.shape[1] // (k * k)
+    oh, ow = out_hw(h, w, k, stride, pad, dil)
+    M = n * oh * ow
+    if M % nseg or M // nseg <= 1:
+        raise ValueError("Expected more than 1 value per channel when training, got input size "
+                         "torch.Size([%d, %d, 1, 1])" % (M // nseg, cout))
+    out = torch.empty((M, cout), dtype=x.dtype, device=x.device)
+    mean = torch.empty((nseg * cout,), dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    nws = int(nv.query("cn_conv_fwd_bn_workspace_floats", dtc(x), M, cout, k * k * cin))
+    ws = torch.empty((nws,), dtype=torch.float32, device=x.device)
+    es = x.element_size()
+    ev = _prof_start(2.0 * M * cout * k * k * cin, ("fwd", M, cout, k * k * cin),
+                     es * (n * h * w * cin + cout * k * k * cin + M * cout))
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    nv.call("cn_conv_fwd_bn", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
+            stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nseg, ws.data_ptr(),
+            mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+            float(mom), float(bn.eps), nv.stream())
+    _prof_end(ev)
+    bn._cn_nbt = getattr(bn, "_cn_nbt", 0) + nseg
+    return out, oh, ow, (mean, invstd)
+
+
+def conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn):
+    """Stride-1 conv input-gradient fused with the backward reduction of the BN + ReLU whose
+    pre-activation x [n*oh*ow, cin] fed the conv (cn_conv_dgrad_bn).  Returns
+    (dy_bn [P, cin], dgamma, dbeta): the gradient at the BN output and the BN's parameter
+    gradients (= the sums cn_bn_bwd_apply needs)."""
+    cout = wt.shape[1] // (k * k)
+    P = n * oh * ow
+    out = torch.empty((P, cin), dtype=dy.dtype, device=dy.device)
+    dgamma = torch.empty((cin,), dtype=torch.float32, device=dy.device)
+    dbeta = torch.empty_like(dgamma)
+    nws = int(nv.query("cn_conv_dgrad_bn_workspace_floats", dtc(dy), P, cin, k * k * cout))
+    ws = torch.empty((nws,), dtype=torch.float32, device=dy.device)
+    es = dy.element_size()
+    ev = _prof_start(2.0 * P * cout * k * k * cin, ("dgrad1", P, cin, k * k * cout),
+                     es * (P * cout + cout * k * k * cin + 2 * P * cin))
+    g, b = _affine(bn)
+    nv.call("cn_conv_dgrad_bn", dtc(dy), dy.data_ptr(), ld(dy), n, oh, ow, cout, wt.data_ptr(), cin,
+            k, k, pad, dil, out.data_ptr(), ld(out), oh, ow, x.data_ptr(), ld(x),
+            stats[0].data_ptr(), stats[1].data_ptr(), nv.ptr(g), nv.ptr(b), dbeta.data_ptr(),
+            dgamma.data_ptr(), ws.data_ptr(), nv.stream())
+    _prof_end(ev)
+    return out, dgamma, dbeta
+
+
+def bn_bwd_apply(x, dy, stats, bn, dgamma, dbeta, out=None):
+    """dx of a train-mode BN + ReLU (mask from x) given its parameter-gradient sums."""
+    p, c = x.shape
+    if out is None:
+        out = torch.empty((p, c), dtype=x.dtype, device=x.device)
+    g, b = _affine(bn)
+    nv.call("cn_bn_bwd_apply", dtc(x), x.data_ptr(), ld(x), dy.data_ptr(), ld(dy), p, c,
+            stats[0].data_ptr(), stats[1].data_ptr(), nv.ptr(g), nv.ptr(b), dbeta.data_ptr(),
+            dgamma.data_ptr(), out.data_ptr(), ld(out), nv.stream())
+    return out
+
+
 def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accumulate=False):
     cout = wt.shape[1] // (k * k)
     if out is None:

@@ -55,6 +55,31 @@ int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, 
 int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                      int accumulate, hipStream_t stream);
 
+/* Conv + train-mode BatchNorm statistics in ONE pass: y = conv2d(x, w) + bias as cn_conv_fwd,
+ * and the GEMM epilogue reduces per-tile column partials of the stored y, so no separate pass
+ * reads y for the statistics (replaces nn.Conv2d + nn.BatchNorm2d's batch-stat reduction of
+ * deeplab/residual_net.py:59-68,:106-107,:129-131 and deeplab/deeplabv3_encoder.py:15-32).
+ * The M = N*OH*OW rows are nseg stacked segments (frames), each its own BN batch: mean / invstd
+ * [nseg][Cout]; running stats updated segment after segment (momentum, eps as nn.BatchNorm2d).
+ * ws: cn_conv_fwd_bn_workspace_floats(dtype, M, Cout, KH*KW*Cin) floats. */
+size_t cn_conv_fwd_bn_workspace_floats(int dtype, int M, int Cout, int K);
+int cn_conv_fwd_bn(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                   const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                   const float* bias, void* y, long long ldy, int OH, int OW, int nseg, float* ws,
+                   float* mean, float* invstd, float* run_mean, float* run_var, float momentum,
+                   float eps, hipStream_t stream);
+/* Conv input-gradient (stride 1) fused with the reduction of the backward of the BN + ReLU that
+ * produced the conv's input (autograd of deeplab/residual_net.py:60-66): dx = dgrad as
+ * cn_conv_dgrad; with x = that BN's input, dz = dx * relu'(bn(x)), sum_dz[c] = sum dz and
+ * sum_dzxh[c] = sum dz * xhat (= the BN's dbeta, dgamma).  Finish with cn_bn_bwd_apply.
+ * ws: cn_conv_dgrad_bn_workspace_floats(dtype, N*H*W, Cin, KH*KW*Cout) floats. */
+size_t cn_conv_dgrad_bn_workspace_floats(int dtype, int M, int Cin, int K);
+int cn_conv_dgrad_bn(int dtype, const void* dy, long long lddy, int N, int OH, int OW, int Cout,
+                     const void* wt, int Cin, int KH, int KW, int pad, int dil, void* dx,
+                     long long lddx, int H, int W, const void* x, long long ldx, const float* mean,
+                     const float* invstd, const float* gamma, const float* beta, float* sum_dz,
+                     float* sum_dzxh, float* ws, hipStream_t stream);
+
 /* Generic batched C = alpha * A . B^T (+bias) with per-operand layouts
  * (0 = k-contiguous rows, 2 = m/n-contiguous, k-major).  Replaces the linear + bmm calls of
  * the co-attention: rgbd_segmentation_RAA.py:159-160,169-170 (RGB) and :212-213,220-221
@@ -91,6 +116,13 @@ int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy, long long
               const float* gamma, const float* beta, int act, const float* prelu, float* dgamma,
               float* dbeta, float* dprelu_c, void* dx, long long lddx, void* dres,
               long long lddres, float* ws, hipStream_t stream);
+
+/* dx of a train-mode BN + ReLU from precomputed sums (cn_conv_dgrad_bn):
+ * dx = gamma*invstd*(dz - sum_dz/P - xhat*sum_dzxh/P), dz = dy * relu'(bn(x)). */
+int cn_bn_bwd_apply(int dtype, const void* x, long long ldx, const void* dy, long long lddy, int P,
+                    int C, const float* mean, const float* invstd, const float* gamma,
+                    const float* beta, const float* sum_dz, const float* sum_dzxh, void* dx,
+                    long long lddx, hipStream_t stream);
 
 /* ---- co-attention softmax (rgbd_segmentation_RAA.py:164-165, :215-216) ----------------- */
 size_t cn_coatt_workspace_floats(int B, int HW, int ld);

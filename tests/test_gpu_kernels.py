@@ -502,3 +502,109 @@ def test_coattention_block(cuda, dt, hw, both):
         got, ref = got.double().cpu(), ref.detach().double()
         err = (got - ref).abs().max().item() / ref.abs().max().item()
         assert err <= tol, (err, tol, tuple(ref.shape))
+
+
+class _BN:
+    """Minimal BatchNorm2d stand-in (the fields ops.* read)."""
+
+    def __init__(self, c, cuda, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.weight = (1 + 0.1 * torch.randn(c, generator=g)).to(cuda)
+        self.bias = (0.1 * torch.randn(c, generator=g)).to(cuda)
+        self.running_mean = torch.zeros(c, device=cuda)
+        self.running_var = torch.ones(c, device=cuda)
+        self.momentum, self.eps, self.affine = 0.1, 1e-5, True
+
+
+FUSED_BN_CASES = [
+    # n (per segment), cin, h, w, cout, k, stride, pad, dil, nseg  (rows straddle M tiles
+    # and the segment boundary at non-multiples of 128; one case with > 2 tiles per segment)
+    (2, 64, 13, 11, 128, 1, 1, 0, 1, 2),
+    (2, 64, 13, 11, 64, 3, 1, 2, 2, 2),
+    (1, 256, 30, 20, 256, 1, 1, 0, 1, 2),
+    (2, 32, 15, 9, 512, 3, 1, 1, 1, 1),
+    (2, 256, 7, 9, 128, 1, 2, 0, 1, 2),
+    (4, 2048, 1, 1, 512, 1, 1, 0, 1, 2),   # the ASPP pooling branch (M = 2 x 4 rows)
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", FUSED_BN_CASES)
+def test_conv_fwd_bn_epilogue_stats(cuda, dt, case):
+    """cn_conv_fwd_bn: conv output + per-segment batch statistics from the GEMM epilogue against
+    torch fp64 conv2d + batch_norm(training=True) per segment (running stats updated in segment
+    order, unbiased running var)."""
+    n, cin, h, w, cout, k, s, p, d, nseg = case
+    x = rnd((nseg * n, cin, h, w), dt, 11, scale=2.0) + 3.0   # non-zero mean: shift exercised
+    wt = rnd((cout, cin, k, k), dt, 12, scale=(2.0 / (cin * k * k)) ** 0.5)
+    bias = rnd((cout,), torch.float32, 13, scale=0.5)
+    ref = F.conv2d(x, wt, bias, s, p, d)
+    bn = _BN(cout, cuda, 14)
+    wf = wt.permute(0, 2, 3, 1).reshape(cout, k * k * cin).to(dt).to(cuda).contiguous()
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    y, oh, ow, (mean, invstd) = ops.conv_fwd_bn(xg, nseg * n, h, w, wf, cout, k, s, p, d, bn, nseg,
+                                                bias=bias.float().to(cuda))
+    torch.cuda.synchronize()
+    close(nchw(y, nseg * n, oh, ow), ref, dt)
+    yr = nchw(y, nseg * n, oh, ow).double().cpu()   # statistics are of the values as stored
+    rm, rv = torch.zeros(cout, dtype=torch.float64), torch.ones(cout, dtype=torch.float64)
+    for sg in range(nseg):
+        ys = yr[sg * n:(sg + 1) * n]
+        mu = ys.mean(dim=(0, 2, 3))
+        var = ys.var(dim=(0, 2, 3), unbiased=False)
+        cnt = ys.numel() // cout
+        assert torch.allclose(mean[sg * cout:(sg + 1) * cout].double().cpu(), mu, atol=1e-4 * (1 + mu.abs().max().item()), rtol=1e-5)
+        assert torch.allclose(invstd[sg * cout:(sg + 1) * cout].double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+        rm = 0.9 * rm + 0.1 * mu
+        rv = 0.9 * rv + 0.1 * var * cnt / (cnt - 1)
+    assert torch.allclose(bn.running_mean.double().cpu(), rm, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn.running_var.double().cpu(), rv, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 0, 1), (2, 64, 13, 11, 64, 3, 2, 2),
+                                  (4, 256, 30, 30, 64, 3, 1, 1), (1, 128, 9, 9, 256, 1, 0, 1)])
+def test_conv_dgrad_bn_epilogue_reduce(cuda, dt, case):
+    """cn_conv_dgrad_bn + cn_bn_bwd_apply: z = relu(bn(xpre)) (train mode) feeds conv(z, w);
+    given dL/dconv_out, the fused dgrad returns dL/dz, dgamma, dbeta and bn_bwd_apply dL/dxpre --
+    against torch fp64 autograd of the same graph."""
+    n, cin, h, w, cout, k, p, d = case
+    xpre = rnd((n, cin, h, w), dt, 21, scale=1.5) + 0.5
+    wt = rnd((cout, cin, k, k), dt, 22, scale=(2.0 / (cin * k * k)) ** 0.5)
+    gy = rnd((n, cout, h, w), dt, 23)
+    bn = _BN(cin, cuda, 24)
+    xr = xpre.clone().requires_grad_(True)
+    gam = bn.weight.double().cpu().requires_grad_(True)
+    bet = bn.bias.double().cpu().requires_grad_(True)
+    z = F.relu(F.batch_norm(xr, None, None, gam, bet, True, 0.1, 1e-5))
+    z.retain_grad()
+    out = F.conv2d(z, wt, None, 1, p, d)
+    out.backward(gy)
+    xg = nhwc(xpre).to(dt).to(cuda).contiguous()
+    mean, invstd = ops.bn_stats(xg, bn, True)
+    wtt = wt.permute(1, 2, 3, 0).reshape(cin, k * k * cout).to(dt).to(cuda).contiguous()
+    dz, dgam, dbet = ops.conv_dgrad_bn(nhwc(gy).to(dt).to(cuda).contiguous(), n, h, w, wtt, cin, k, p, d,
+                                       xg, (mean, invstd), bn)
+    dx = ops.bn_bwd_apply(xg, dz, (mean, invstd), bn, dgam, dbet)
+    # the unfused HIP path on the same stored dy: dgrad, then the BN backward's own reduce + apply
+    dz2 = ops.conv_dgrad(nhwc(gy).to(dt).to(cuda).contiguous(), n, h, w, wtt, cin, k, 1, p, d, h, w)
+    dx2, dgam2, dbet2, _ = ops.bn_bwd(xg, dz2, None, (mean, invstd), bn, act=1)
+    torch.cuda.synchronize()
+    close(nchw(dz, n, h, w), z.grad, dt)
+    assert torch.equal(dz, dz2)
+    # fused == unfused up to the order of the fp32 sums (and one output rounding of dx)
+    for a, b, t in ((dgam, dgam2, 1e-5), (dbet, dbet2, 1e-5),
+                    (dx.float(), dx2.float(), 1e-5 if dt == torch.float32 else 8e-3)):
+        assert ((a - b).abs().max() / b.abs().max()).item() <= t
+    if dt == torch.float32:
+        for got, ref in ((dgam, gam.grad), (dbet, bet.grad), (nchw(dx, n, h, w), xr.grad)):
+            got, ref = got.double().cpu(), ref.double()
+            assert (got - ref).abs().max().item() / ref.abs().max().item() <= 1e-4
+    else:
+        # bf16: the ReLU mask of a bf16-rounded pre-activation flips where bn(x) ~ 0, and one flip
+        # is a full-size error in max-abs terms: dgamma max-rel, dx / dbeta mean-abs
+        g, r = dgam.double().cpu(), gam.grad.double()
+        assert (g - r).abs().max().item() / r.abs().max().item() <= 1e-2
+        for got, ref in ((dbet, bet.grad), (nchw(dx, n, h, w), xr.grad)):
+            got, ref = got.double().cpu(), ref.double()
+            assert (got - ref).abs().mean().item() <= 2e-2 * ref.abs().mean().item()
