@@ -47,6 +47,11 @@ _SIGS = {
     "cn_coatt_softmax": (_I, [_I, _P, _I, _I, _I, _P, _P, _P, _P]),
     "cn_coatt_dscore": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "cn_coatt_fused_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P]),
+    "cn_coatt_flash_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P]),
+    "cn_coatt_flash_pv": (_I, [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _P, _L, _I, _P]),
+    "cn_coatt_flash_dvat": (_I, [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _I, _I, _I, _P,
+                                 _L, _I, _P]),
+    "cn_rowdot_seg": (_I, [_I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _P]),
     "cn_nchw_to_nhwc": (_I, [_I, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cn_weight_prep": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P]),
     "cn_maxpool_fwd": (_I, [_I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -64,10 +64,13 @@ __device__ __forceinline__ void raw_barrier_f() {
 struct FusedDir {
   const bf16* q; const bf16* k; const bf16* v; bf16* o;
   long long ldq, ldk, ldv, ldo;
+  float* lse;          // MODE 0 (optional): log2-sum-exp2 of each query row's logits x log2(e),
+                       //   [B][HWp] (rows HW..HWp-1 get +inf)
+  const float* klse;   // MODE 1: per-KEY normaliser in the same units, [B][HWp], +inf padded
 };
 struct FusedArgs {
   FusedDir dir[2];
-  int HW, ndir, nrb, nwork;
+  int HW, HWp, ndir, nrb, nwork, accumulate;
 };
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
@@ -88,6 +91,11 @@ __device__ __forceinline__ bf16x8 pack8(const float* f) {
   return r;
 }
 
+// MODE 0: softmax over the keys of each query row (online max / sum), O = P V / l.
+// MODE 1: P[q][k] = exp2(S[q][k] log2e - klse[k]) with a per-KEY normaliser computed by an
+//         earlier MODE 0 pass in the other direction (no max, no sum), O (+)= P V.  This is the
+//         co-attention backward's dV_a = P_row dZ_b (rgbd_segmentation_RAA.py:169 autograd).
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void coatt_fused_fwd_k(FusedArgs a) {
   // [Q: 128 rows x 512 B][stage 0: K | V][stage 1: K | V][stage 2: K | V]   (64 + 3 x 32 KB)
@@ -177,6 +185,14 @@ void coatt_fused_fwd_k(FusedArgs a) {
     st2 = st2 == FSTAGES - 1 ? 0 : st2 + 1;
     const char* vb = kb + FTILE;
 
+    // MODE 1: this tile's per-key normalisers (lane's keys 32t + 8q + 4h + 0..3), loaded ahead
+    // of the S MFMAs so their latency hides under them
+    f32x4 nk[4];
+    if constexpr (MODE == 1) {
+      const float* kl = d.klse + b * a.HWp + t * FBK + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nk[q] = *(const f32x4*)(kl + 8 * q);
+    }
     // ---- S^T tile (32 keys x 32 query rows per wave) = K Q^T over 16 k-steps of d;
     // both fragments come from LDS, read KPF steps ahead
     f32x16 s = f32x16{};
@@ -239,6 +255,19 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
     // ---- online softmax over the keys (register i: key 32t + (i&3) + 8(i>>2) + 4h)
     const int key0 = t * FBK;
+    bf16x8 pf[2];
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * s2 + j;
+          pv[j] = __builtin_amdgcn_exp2f(fmaf(s[i], L2E, -nk[i >> 2][i & 3]));
+        }
+        pf[s2] = pack8(pv);
+      }
+    } else {
     if (key0 + FBK > HW) {
 #pragma unroll
       for (int i = 0; i < 16; ++i)
@@ -260,7 +289,6 @@ void coatt_fused_fwd_k(FusedArgs a) {
         for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
       m = mnew;
     }
-    bf16x8 pf[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       float pv[8];
@@ -271,6 +299,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
       }
       pf[s2] = pack8(pv);
     }
+    }  // MODE 0
 
     // ---- O^T += V^T P^T: k-step sk covers keys 16 sk .. +15 in the accumulator's k order;
     // 16 (dt, sk) steps, V^T fragments read VPF steps ahead.  The transposed reads are inline
@@ -316,8 +345,10 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
   // ---- epilogue: O[qrow][d] = o / l ; register i of d tile dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
   l += __shfl_xor(l, 32, 64);
+  if (MODE == 0 && d.lse && h == 0 && qrow < a.HWp)
+    d.lse[b * a.HWp + qrow] = qrow < HW ? m + __builtin_amdgcn_logf(l) : INFINITY;  // logf = log2
   if (qrow < HW) {
-    const float inv = 1.f / l;
+    const float inv = MODE == 0 ? 1.f / l : 1.f;
     bf16* op = d.o + (b * HW + qrow) * d.ldo + 4 * h;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
@@ -325,8 +356,14 @@ void coatt_fused_fwd_k(FusedArgs a) {
       for (int c = 0; c < 4; ++c) {
         typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
         bf16x4 v;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + 32 * dt + 8 * c);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv + (float)old[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+        }
         *(bf16x4*)(op + 32 * dt + 8 * c) = v;
       }
   }
@@ -336,27 +373,65 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
+  a.ndir = nd;
+  a.nrb = (a.HW + FBQ - 1) / FBQ;
+  a.nwork = a.nrb * B * nd;
+  dim3 grid(((a.nwork + 7) / 8) * 8);
+  if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+static int fused_check(const void* q, long long ldq, const void* k, long long ldk, const void* v,
+                       long long ldv, long long ldo, int C) {
+  if (C != FD) return CN_ERR_SHAPE;
+  if (ldq % 8 || ldk % 8 || ldv % 8 || ldo % 4 || ldq < C || ldk < C || ldv < C || ldo < C)
+    return CN_ERR_ALIGN;
+  if (!aligned16(q) || !aligned16(k) || !aligned16(v)) return CN_ERR_ALIGN;
+  return 0;
+}
+
 extern "C" int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
                                   const void* vb, long long ld_vb, int B, int HW, int C, void* za,
                                   void* zb, long long ld_z, hipStream_t st) {
-  if (C != FD || B <= 0 || HW <= 0) return CN_ERR_SHAPE;
-  if (ld_vat % 8 || ld_va % 8 || ld_vb % 8 || ld_z % 4 || ld_vat < C || ld_va < C || ld_vb < C || ld_z < C)
-    return CN_ERR_ALIGN;
-  if (!aligned16(vat) || !aligned16(va) || !aligned16(vb) || ((uintptr_t)za & 7) || ((uintptr_t)zb & 7))
-    return CN_ERR_ALIGN;
-  FusedArgs a;
+  return cn_coatt_flash_fwd(vat, ld_vat, va, ld_va, vb, ld_vb, B, HW, C, za, zb, ld_z, nullptr,
+                            nullptr, st);
+}
+
+extern "C" int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                  const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                                  void* zb, long long ld_z, float* lse_a, float* lse_b,
+                                  hipStream_t st) {
+  if (B <= 0 || HW <= 0) return CN_ERR_SHAPE;
+  int rc = fused_check(vat, ld_vat, vb, ld_vb, va, ld_va, ld_z, C);
+  if (rc) return rc;
+  if (((uintptr_t)za & 7) || ((uintptr_t)zb & 7)) return CN_ERR_ALIGN;
+  FusedArgs a = {};
   int nd = 0;
   // direction 0: Z_a = softmax_j(S) Vb  (queries i: Va_t; keys j: Vb; values Vb)
-  if (za) a.dir[nd++] = FusedDir{(const bf16*)vat, (const bf16*)vb, (const bf16*)vb, (bf16*)za, ld_vat, ld_vb, ld_vb, ld_z};
+  if (za) a.dir[nd++] = FusedDir{(const bf16*)vat, (const bf16*)vb, (const bf16*)vb, (bf16*)za, ld_vat, ld_vb, ld_vb, ld_z, lse_a, nullptr};
   // direction 1: Z_b = softmax_i(S)^T Va  (queries j: Vb; keys i: Va_t; values Va)
-  if (zb) a.dir[nd++] = FusedDir{(const bf16*)vb, (const bf16*)vat, (const bf16*)va, (bf16*)zb, ld_vb, ld_vat, ld_va, ld_z};
+  if (zb) a.dir[nd++] = FusedDir{(const bf16*)vb, (const bf16*)vat, (const bf16*)va, (bf16*)zb, ld_vb, ld_vat, ld_va, ld_z, lse_b, nullptr};
   if (nd == 0) return CN_ERR_SHAPE;
   a.HW = HW;
-  a.ndir = nd;
-  a.nrb = (HW + FBQ - 1) / FBQ;
-  a.nwork = a.nrb * B * nd;
-  dim3 grid(((a.nwork + 7) / 8) * 8);
-  hipLaunchKernelGGL(coatt_fused_fwd_k, grid, dim3(256), 0, st, a);
-  CN_CHECK_LAUNCH();
-  return 0;
+  a.HWp = (HW + 31) / 32 * 32;
+  a.accumulate = 0;
+  return fused_launch(0, a, B, nd, st);
+}
+
+extern "C" int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk,
+                                 const void* v, long long ldv, const float* klse, int B, int HW,
+                                 int C, void* o, long long ldo, int accumulate, hipStream_t st) {
+  if (B <= 0 || HW <= 0 || !klse || !o) return CN_ERR_SHAPE;
+  int rc = fused_check(q, ldq, k, ldk, v, ldv, ldo, C);
+  if (rc) return rc;
+  if (((uintptr_t)o & 7) || ((uintptr_t)klse & 15)) return CN_ERR_ALIGN;
+  FusedArgs a = {};
+  a.dir[0] = FusedDir{(const bf16*)q, (const bf16*)k, (const bf16*)v, (bf16*)o, ldq, ldk, ldv, ldo, nullptr, klse};
+  a.HW = HW;
+  a.HWp = (HW + 31) / 32 * 32;
+  a.accumulate = accumulate;
+  return fused_launch(1, a, B, 1, st);
 }

@@ -662,7 +662,7 @@ __global__ __launch_bounds__(256) void sgd_k(const SgdTensor* __restrict__ ts, i
 // ---- generic helpers ------------------------------------------------------------------
 template <class T>
 __global__ void rowdot_k(const T* __restrict__ a, long long lda, const T* __restrict__ b,
-                         long long ldb, int P, int C, float* __restrict__ out) {
+                         long long ldb, int P, int C, int seg, int seg_ld, float* __restrict__ out) {
   constexpr int V = VecOf<T>::N;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -676,7 +676,7 @@ __global__ void rowdot_k(const T* __restrict__ a, long long lda, const T* __rest
     for (int v = 0; v < V; ++v) acc = fmaf(f[v], q[v], acc);
   }
   acc = warp_sum(acc);
-  if (lane == 0) out[row] = acc;
+  if (lane == 0) out[(long long)(row / seg) * seg_ld + row % seg] = acc;
 }
 
 // column sums of T [P][C] (ld) into fp32 [C] (atomic across row blocks)
@@ -997,15 +997,21 @@ extern "C" int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, f
   return 0;
 }
 
-extern "C" int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb,
-                         int P, int C, float* out, hipStream_t st) {
+extern "C" int cn_rowdot_seg(int dtype, const void* a, long long lda, const void* b, long long ldb,
+                             int P, int C, int seg, int seg_ld, float* out, hipStream_t st) {
+  if (seg < 1 || seg_ld < seg) return CN_ERR_SHAPE;
   dim3 grid((P + 3) / 4);
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(rowdot_k<bf16>, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, P, C, out);
+    hipLaunchKernelGGL(rowdot_k<bf16>, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, P, C, seg, seg_ld, out);
   else
-    hipLaunchKernelGGL(rowdot_k<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, P, C, out);
+    hipLaunchKernelGGL(rowdot_k<float>, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, P, C, seg, seg_ld, out);
   CN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb,
+                         int P, int C, float* out, hipStream_t st) {
+  return cn_rowdot_seg(dtype, a, lda, b, ldb, P, C, P > 0 ? P : 1, P > 0 ? P : 1, out, st);
 }
 
 extern "C" int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out, float* ws,

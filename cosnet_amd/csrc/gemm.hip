@@ -287,7 +287,7 @@ __device__ __forceinline__ void raw_barrier() {
 // blocks per CU, the
 // occupancy the plain kernel has from its LDS footprint; HIP's 2nd bound is waves per SIMD).
 template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0>
-__global__ __launch_bounds__(WM * WN * 64, (EPI && BM * BN <= 128 * 128) ? 4 : 1) void gemm_kernel(GemmArgs p) {
+__global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128) ? 4 : 1) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
   constexpr int VEC = VecOf<T>::N;
   constexpr int BK = 8 * VEC;

@@ -271,12 +271,22 @@ class CoattFn(F):
         vat = ops.gemm(va, wf, n * hw, c, c, lda=ops.ld(va), ldb=c)            # :158-159
         ctx.geo = (n, hw, c, ldp)
         ctx.set_materialize_grads(False)
-        if not _need(ctx) and ops.coatt_fused_ok(dt, c, va, vb):
-            # inference: both directions in one flash-style launch, S never leaves the chip
+        if ops.coatt_fused_ok(dt, c, va, vb):
+            # both directions in one flash-style launch, S never leaves the chip
             za = torch.empty((n * hw, c), dtype=dt, device=dev)
             zb = torch.empty((n * hw, c), dtype=dt, device=dev)
-            ops.coatt_fused(vat, va, vb, n, hw, za, zb)                          # :160-170
+            if not _need(ctx):                                                   # inference
+                ops.coatt_fused(vat, va, vb, n, hw, za, zb)                      # :160-170
+                return za, zb
+            # training: keep the per-row normalisers; the backward recomputes P from them
+            lse_a = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=dev)
+            lse_b = torch.empty_like(lse_a)
+            ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)       # :160-170
+            ctx.s = (va, vb, wf, vat, za, zb, lse_a, lse_b)
+            ctx.flash = True
+            ctx.link = link
             return za, zb
+        ctx.flash = False
         S = torch.empty((n, hw, ldp), dtype=torch.float32, device=dev)
         ops.gemm(vat, vb, hw, hw, c, lda=c, ldb=ops.ld(vb), a_bs=hw * c, b_bs=hw * ops.ld(vb),
                  out=S, ldc=ldp, c_bs=hw * ldp, batch=n, tag="affinity")          # :160
@@ -298,6 +308,8 @@ class CoattFn(F):
 
     @staticmethod
     def backward(ctx, dza, dzb):
+        if ctx.flash:
+            return CoattFn._flash_backward(ctx, dza, dzb)
         va, vb, wf, pc, pt, za, zb = ctx.s
         n, hw, c, ldp = ctx.geo
         dt = va.dtype
@@ -344,6 +356,47 @@ class CoattFn(F):
                 ops.gemm(pt, dzb, hw, c, hw, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=ldp,
                          ldb=c, a_bs=hw * ldp, b_bs=hw * c, out=dva, ldc=c, c_bs=hw * c, batch=n,
                          c_mode=mode)
+                mode = 2
+            # dVa += dVa_t . W   (B[n=ci][k=co] = W[co][ci] -> MC)
+            ops.gemm(dvat, wf, P, c, c, layout_b=ops.GEMM_MC, lda=c, ldb=c, out=dva, ldc=c,
+                     c_mode=mode)
+        dw = None
+        if ctx.needs_input_grad[2]:
+            dw = torch.empty((c, c), dtype=torch.float32, device=dev)
+            ns = max(1, min(64, P // 512))
+            ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
+                     ldb=ops.ld(va), out=dw, ldc=c, c_mode=0, nsplit=ns)
+        return dva, None, dw, None, None
+
+    @staticmethod
+    def _flash_backward(ctx, dza, dzb):
+        """Flash backward (coatt_flash.hip): dS never materialised.
+          dVa_t = sum_j dS[i][j] Vb[j]                (cn_coatt_flash_dvat)
+          dV_a  = [link] + sum_j P1[i][j] dZb[j]       (cn_coatt_flash_pv, S_row . dZ_b)
+                  + dVa_t W                           (GEMM, the linear's input gradient)
+          dW    = dVa_t^T V_a                         (GEMM, the linear's weight gradient)"""
+        va, vb, wf, vat, za, zb, lse_a, lse_b = ctx.s
+        n, hw, c, _ = ctx.geo
+        dt = va.dtype
+        dev = va.device
+        P = n * hw
+        dv_link = ctx.link.pop("dv", None) if ctx.link is not None else None
+        if dza is None and dzb is None:
+            return dv_link, None, None, None, None
+        dza = dza.contiguous() if dza is not None else None
+        dzb = dzb.contiguous() if dzb is not None else None
+        need_va = ctx.needs_input_grad[0]
+        dva = None
+        mode = 0
+        if need_va:
+            dva = torch.empty((P, c), dtype=dt, device=dev)
+            if dv_link is not None:
+                ops.cast_copy(dv_link, dva)
+                mode = 2
+        dvat = ops.coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw,
+                                   dva=dva, dva_accumulate=mode == 2)
+        if need_va:
+            if dzb is not None:
                 mode = 2
             # dVa += dVa_t . W   (B[n=ci][k=co] = W[co][ci] -> MC)
             ops.gemm(dvat, wf, P, c, c, layout_b=ops.GEMM_MC, lda=c, ldb=c, out=dva, ldc=c,

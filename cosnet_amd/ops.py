@@ -372,6 +372,59 @@ def coatt_fused(vat, va, vb, n, hw, za=None, zb=None):
     return za, zb
 
 
+def hw_pad(hw):
+    return (hw + 31) // 32 * 32
+
+
+def coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b):
+    """Training forward of both co-attention directions (S never in HBM) + the per-row
+    log2-sum-exp2 normalisers [n, hw_pad(hw)] the backward recomputes P from."""
+    c = vat.shape[1]
+    ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_flash_fwd", n, hw, c),
+                     (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
+    nv.call("cn_coatt_flash_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
+            ld(vb), n, hw, c, za.data_ptr(), zb.data_ptr(), ld(za), lse_a.data_ptr(),
+            lse_b.data_ptr(), nv.stream())
+    _prof_end(ev)
+
+
+def coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw, dva=None,
+                    dva_accumulate=False):
+    """Backward of the flash co-attention: returns dVa_t [P, C] (bf16) and, if `dva` is given,
+    accumulates dV_a's softmax-over-i term sum_j P1[i][j] dZ_b[j] into it.  Algorithmic work
+    (the reference's autograd): 4 x 2 HW^2 C per pair with both gradients."""
+    c = vat.shape[1]
+    P = n * hw
+    hwp = hw_pad(hw)
+    dev = vat.device
+    d0 = d1 = None
+    if dza is not None:
+        d0 = torch.empty((P,), dtype=torch.float32, device=dev)
+        nv.call("cn_rowdot", dtc(dza), dza.data_ptr(), ld(dza), za.data_ptr(), ld(za), P, c,
+                d0.data_ptr(), nv.stream())
+    if dzb is not None:
+        d1 = torch.empty((n * hwp,), dtype=torch.float32, device=dev)
+        nv.call("cn_rowdot_seg", dtc(dzb), dzb.data_ptr(), ld(dzb), zb.data_ptr(), ld(zb), P, c, hw,
+                hwp, d1.data_ptr(), nv.stream())
+    dvat = torch.empty((P, c), dtype=vat.dtype, device=dev)
+    nterm = (dza is not None) + (dzb is not None)
+    ev = _prof_start((1 + 2 * nterm) * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
+                     (2 + 2 * nterm) * P * c * vat.element_size())
+    nv.call("cn_coatt_flash_dvat", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), nv.ptr(dza),
+            ld(dza) if dza is not None else c, vb.data_ptr(), ld(vb), nv.ptr(dzb),
+            ld(dzb) if dzb is not None else c, lse_a.data_ptr(), nv.ptr(d0), lse_b.data_ptr(),
+            nv.ptr(d1), n, hw, c, dvat.data_ptr(), ld(dvat), 0, nv.stream())
+    _prof_end(ev)
+    if dva is not None and dzb is not None:
+        ev = _prof_start(2 * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
+                         3 * P * c * vat.element_size())
+        nv.call("cn_coatt_flash_pv", vat.data_ptr(), ld(vat), vb.data_ptr(), ld(vb), dzb.data_ptr(),
+                ld(dzb), lse_b.data_ptr(), n, hw, c, dva.data_ptr(), ld(dva), int(dva_accumulate),
+                nv.stream())
+        _prof_end(ev)
+    return dvat
+
+
 def _nsplit_eff(k, nsplit, dt):
     """Number of splits cn_gemm really launches (chunks rounded up to whole K tiles)."""
     bk = 64 if dt == torch.bfloat16 else 32

@@ -140,6 +140,33 @@ int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long l
                        const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                        long long ld_z, hipStream_t stream);
 
+/* Flash-style co-attention for TRAINING (rgbd_segmentation_RAA.py:160-170 and its autograd),
+ * S never in HBM.  Forward = cn_coatt_fused_fwd plus the per-row log2-sum-exp2 of each direction
+ * (lse_a[b][i] over j of S[i][j] log2(e), lse_b[b][j] over i), [B][HWp] with HWp = HW rounded up
+ * to 32 and +inf in the padding; either may be NULL. */
+int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                       const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                       long long ld_z, float* lse_a, float* lse_b, hipStream_t stream);
+/* o[q] (+)= sum_k exp2(q.k log2(e) - klse[k]) v[k]: a softmax product whose normaliser is per
+ * KEY (the other direction's lse) -- the co-attention backward's dV_a = S_row dZ_b
+ * (autograd of rgbd_segmentation_RAA.py:169) with q = Va_t, k = Vb, v = dZ_b, klse = lse_b.
+ * bf16, C == 256; accumulate: o += result (bf16 read-add-write). */
+int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk, const void* v,
+                      long long ldv, const float* klse, int B, int HW, int C, void* o, long long ldo,
+                      int accumulate, hipStream_t stream);
+
+/* Backward of the flash co-attention: dva_t (+)= sum_j dS[i][j] vb[j] with
+ *   dS = P0 (dza[i].vb[j] - d0[i]) + P1 (va[i].dzb[j] - d1[j]),
+ *   P0 = exp2(S log2e - lse_a[i]), P1 = exp2(S log2e - lse_b[j]), S = vat vb^T,
+ * d0 = rowdot(dza, za) [B][HW], d1 = rowdot(dzb, zb) at [B][HWp].  dza == NULL drops the P0 term,
+ * dzb == NULL the P1 term (a direction that receives no gradient).  bf16, C == 256.
+ * Replaces the autograd of rgbd_segmentation_RAA.py:160-170 (with cn_coatt_flash_pv for dV_a). */
+int cn_coatt_flash_dvat(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                        const void* dza, long long ld_dza, const void* vb, long long ld_vb,
+                        const void* dzb, long long ld_dzb, const float* lse_a, const float* d0,
+                        const float* lse_b, const float* d1, int B, int HW, int C, void* out,
+                        long long ld_out, int accumulate, hipStream_t stream);
+
 /* ---- memory-bound helpers -------------------------------------------------------------- */
 int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* y,
                     hipStream_t stream);
@@ -206,6 +233,9 @@ int cn_sgd(const void* tensors, int nt, const float* lrs, float wd, float moment
            hipStream_t stream);
 int cn_rowdot(int dtype, const void* a, long long lda, const void* b, long long ldb, int P, int C,
               float* out, hipStream_t stream);
+/* rowdot with the rows in segments of `seg` written at a stride of seg_ld (padded per pair) */
+int cn_rowdot_seg(int dtype, const void* a, long long lda, const void* b, long long ldb, int P, int C,
+                  int seg, int seg_ld, float* out, hipStream_t stream);
 int cn_colsum(int dtype, const void* x, long long ld, int P, int C, float* out,
               float* ws /* cn_colpart_workspace_floats(P, C) */, hipStream_t stream);
 int cn_cast2d(int dtype_in, int dtype_out, const void* x, long long ldx, int P, int C, void* y,

@@ -114,3 +114,49 @@ def test_coattfn_inference_uses_fused_and_matches_materialised(cuda, monkeypatch
     torch.cuda.synchronize()
     assert len(calls) == 1
     assert rel(fa, ma.double()) <= TOL and rel(fb, mb.double()) <= TOL, (rel(fa, ma.double()), rel(fb, mb.double()))
+
+
+@pytest.mark.parametrize("n,hw", [(1, 97), (2, 169), (2, 1271), (4, 3600)])
+@pytest.mark.parametrize("which", ["both", "a_only", "b_only"])
+def test_flash_training_fwd_bwd_vs_fp64(cuda, n, hw, which):
+    """CoattFn's training path in bf16 (flash forward with LSE + flash backward: S, P and dS never
+    in HBM) against fp64 autograd of rgbd_segmentation_RAA.py:158-170 on the same bf16 inputs.
+    which: gradient reaching Z_a only / Z_b only / both (the depth block's Z_b gets none).
+    Tolerance 3e-2 of each output's scale (P, dS rounded to bf16 as the materialised path does)."""
+    from cosnet_amd.functions import CoattFn
+    c = 256
+    g = torch.Generator().manual_seed(hw + n)
+    va = (torch.randn((n * hw, c), generator=g) * 0.7).to(torch.bfloat16)
+    vb = (torch.randn((n * hw, c), generator=g) * 0.7).to(torch.bfloat16)
+    W = torch.randn((c, c), generator=g) * c ** -0.5
+    ga = torch.randn((n * hw, c), generator=g).to(torch.bfloat16)
+    gb = torch.randn((n * hw, c), generator=g).to(torch.bfloat16)
+    # fp64 reference on the device (test arithmetic)
+    var = va.double().to(cuda).requires_grad_(True)
+    wr = W.double().to(cuda).requires_grad_(True)
+    vat = (var @ wr.t()).reshape(n, hw, c)
+    b3 = vb.double().to(cuda).reshape(n, hw, c)
+    S = vat @ b3.transpose(1, 2)
+    za_r = (torch.softmax(S, 2) @ b3).reshape(n * hw, c)
+    zb_r = (torch.softmax(S, 1).transpose(1, 2) @ var.reshape(n, hw, c)).reshape(n * hw, c)
+    outs, grads = [], []
+    if which in ("both", "a_only"):
+        outs.append(za_r); grads.append(ga.double().to(cuda))
+    if which in ("both", "b_only"):
+        outs.append(zb_r); grads.append(gb.double().to(cuda))
+    torch.autograd.backward(outs, grads)
+    # HIP flash path
+    vag = va.to(cuda).requires_grad_(True)
+    Wg = torch.nn.Parameter(W.to(cuda))
+    za, zb = CoattFn.apply(vag, vb.to(cuda), Wg, (n, hw))
+    outs, grads = [], []
+    if which in ("both", "a_only"):
+        outs.append(za); grads.append(ga.to(cuda))
+    if which in ("both", "b_only"):
+        outs.append(zb); grads.append(gb.to(cuda))
+    torch.autograd.backward(outs, grads)
+    torch.cuda.synchronize()
+    for name, got, ref in (("Z_a", za, za_r), ("Z_b", zb, zb_r), ("dV_a", vag.grad, var.grad),
+                           ("dW", Wg.grad, wr.grad)):
+        e = rel(got, ref.detach())
+        assert e <= 3e-2, (name, e)
