@@ -36,7 +36,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4, help="frame pairs per GPU")
     ap.add_argument("--size", type=int, default=473)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: e4m3 operands for the encoders' forward conv GEMMs (BASELINE "
+                         "configs[4]; bf16 everywhere else)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
@@ -181,10 +183,12 @@ def main():
     from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
     from cosnet_amd.train_step import TrainStep
 
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = torch.float32 if args.dtype == "fp32" else torch.bfloat16
     torch.manual_seed(1234)
     model = C.build_model(dtype)
     model.load_state_dict(recipe_state_dict(model.state_dict()))
+    if args.dtype == "fp8":
+        model.set_fp8(True)
     # encoder.main_classifier only produces `labels`, which never enters the loss
     # (SURVEY.md §3.3): it receives no gradient in the reference either.
     model.encoder.main_classifier.requires_grad_(False)

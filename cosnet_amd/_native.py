@@ -29,6 +29,11 @@ _SIGS = {
     "cn_conv_wgrad_workspace_floats": (_S, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "cn_conv_wgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cn_splitk_reduce": (_I, [_P, _I, _L, _L, _P, _I, _P]),
+    "cn_fp8_quant": (_I, [_I, _P, _L, _I, _I, _P, _L, _P, _I, _P]),
+    "cn_fp8_update": (_I, [_P, _I, _F, _P]),
+    "cn_fp8_quant_multi": (_I, [_P, _I, _P]),
+    "cn_conv_fwd_fp8": (_I, [_P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I, _P,
+                             _P, _P]),
     "cn_conv_fwd_bn_workspace_floats": (_S, [_I, _I, _I, _I]),
     "cn_conv_fwd_bn": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I,
                             _I, _P, _P, _P, _P, _P, _F, _F, _P]),
@@ -41,6 +46,8 @@ _SIGS = {
     "cn_bn_stats": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P]),
     "cn_bn_eval_params": (_I, [_P, _P, _I, _F, _P, _P, _P]),
     "cn_bn_apply": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P, _P, _L, _P]),
+    "cn_bn_apply_fp8": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P,
+                             _P, _L, _P, _L, _P, _P]),
     "cn_bn_set_tuning": (_I, [_I, _I]),
     "cn_bn_bwd": (_I, [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P]),
     "cn_coatt_workspace_floats": (_S, [_I, _I, _I]),

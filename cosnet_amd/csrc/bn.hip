@@ -293,6 +293,29 @@ __global__ void bn_eval_params(const float* rm, const float* rv, int C, float ep
   invstd[c] = 1.0f / sqrtf(rv[c] + eps);
 }
 
+// fp8 e4m3 (OCP) packing of the optional fp8 output of bn_apply (cosnet_amd/fp8.py): saturating
+__device__ __forceinline__ unsigned pack4_fp8_bn(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  unsigned w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+
+// amax of the block -> one atomicMax on the state's amax slot (every thread must call)
+__device__ __forceinline__ void fp8_block_amax(float m, float* state) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+    if (m > 0.f) atomicMax((unsigned*)&state[2], __float_as_uint(m));
+  }
+}
+
 // V consecutive fp32 per-channel constants (16-byte aligned; null -> dflt)
 template <int V>
 __device__ __forceinline__ void ld_params(const float* p, int c0, float dflt, float* o) {
@@ -318,12 +341,18 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
                                                   const float* rmean, const float* rinvstd,
                                                   const float* rgamma, const float* rbeta, int act,
                                                   const float* prelu, T* __restrict__ y,
-                                                  long long ldy) {
+                                                  long long ldy, unsigned char* __restrict__ y8,
+                                                  long long ldy8, float* qstate) {
   constexpr int V = VecOf<T>::N;
   const Layout L = layout_of<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
-  if (chunk >= L.CPR || ty >= L.RPB) return;
+  float qmax = 0.f;
+  const float qinv = y8 ? qstate[1] : 0.f;
+  if (chunk >= L.CPR || ty >= L.RPB) {
+    if (y8) fp8_block_amax(qmax, qstate);
+    return;
+  }
   const int seg = blockIdx.z, c0 = chunk * V;
   const long long row0 = (long long)seg * P;
   float sc[V], sf[V], rsc[V], rsf[V], t0[V], t1[V];
@@ -373,8 +402,20 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         f[u][v] = t;
       }
       st_chunk(y + r * ldy + c0, f[u]);
+      if (y8) {  // fp8 copy of the output for an fp8 consumer conv (delayed scaling)
+#pragma unroll
+        for (int v = 0; v < V; ++v) qmax = fmaxf(qmax, fabsf(f[u][v]));
+#pragma unroll
+        for (int v = 0; v < V; v += 8) {
+          u32x2 o;
+          o.x = pack4_fp8_bn(f[u][v] * qinv, f[u][v + 1] * qinv, f[u][v + 2] * qinv, f[u][v + 3] * qinv);
+          o.y = pack4_fp8_bn(f[u][v + 4] * qinv, f[u][v + 5] * qinv, f[u][v + 6] * qinv, f[u][v + 7] * qinv);
+          *(u32x2*)(y8 + r * ldy8 + c0 + v) = o;
+        }
+      }
     }
   }
+  if (y8) fp8_block_amax(qmax, qstate);
 }
 
 // ---- backward reduce: planes sum(dz), sum(dz * xhat) [, sum(dz * pre * (pre<=0)) PReLU] ----
@@ -662,12 +703,32 @@ extern "C" int cn_bn_eval_params(const float* run_mean, const float* run_var, in
   return 0;
 }
 
+extern "C" int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                               const float* mean, const float* invstd, const float* gamma,
+                               const float* beta, const void* res, long long ldr, const void* xr,
+                               long long ldxr, const float* rmean, const float* rinvstd,
+                               const float* rgamma, const float* rbeta, int act, const float* prelu,
+                               void* y, long long ldy, void* y8, long long ldy8, float* qstate,
+                               hipStream_t st);
+
 extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int nseg, int C,
                            const float* mean, const float* invstd, const float* gamma,
                            const float* beta, const void* res, long long ldr, const void* xr,
                            long long ldxr, const float* rmean, const float* rinvstd,
                            const float* rgamma, const float* rbeta, int act, const float* prelu,
                            void* y, long long ldy, hipStream_t st) {
+  return cn_bn_apply_fp8(dtype, x, ldx, P, nseg, C, mean, invstd, gamma, beta, res, ldr, xr, ldxr,
+                         rmean, rinvstd, rgamma, rbeta, act, prelu, y, ldy, nullptr, 0, nullptr, st);
+}
+
+extern "C" int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                               const float* mean, const float* invstd, const float* gamma,
+                               const float* beta, const void* res, long long ldr, const void* xr,
+                               long long ldxr, const float* rmean, const float* rinvstd,
+                               const float* rgamma, const float* rbeta, int act, const float* prelu,
+                               void* y, long long ldy, void* y8, long long ldy8, float* qstate,
+                               hipStream_t st) {
+  if (y8 && (dtype != DT_BF16 || !qstate || ldy8 % 16 || ((uintptr_t)y8 & 7))) return CN_ERR_ALIGN;
   const int vec = dtype == DT_BF16 ? 8 : 4;
   if (C % vec || ldx % vec || ldy % vec || (res && ldr % vec) || (xr && ldxr % vec)) return CN_ERR_ALIGN;
   if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
@@ -679,12 +740,14 @@ extern "C" int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int n
     gy = grid_rows<bf16>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
     hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy, nseg), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
-                       rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy);
+                       rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy, (unsigned char*)y8, ldy8,
+                       qstate);
   } else {
     gy = grid_rows<float>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
     hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy, nseg), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
-                       rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy);
+                       rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy,
+                       (unsigned char*)nullptr, 0ll, (float*)nullptr);
   }
   CN_CHECK_LAUNCH();
   return 0;

@@ -85,6 +85,23 @@ static int conv_fwd_args(int dtype, const void* x, long long ldx, int N, int H, 
   return 0;
 }
 
+// y (bf16) = conv2d(x8, w8) * x_scale * w_scale (+ bias): fp8 e4m3 operands (cn_fp8_quant), fp32
+// accumulation on the block-scaled 16x16x128 MFMA, per-tensor dequantisation in the epilogue.
+extern "C" int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin,
+                               const void* w8, int Cout, int KH, int KW, int stride, int pad, int dil,
+                               const float* bias, void* y, long long ldy, int OH, int OW,
+                               const float* x_state, const float* w_state, hipStream_t st) {
+  if (Cin % 16 || ldx % 16 || ((uintptr_t)x8 & 15) || ((uintptr_t)w8 & 15)) return CN_ERR_ALIGN;
+  GemmArgs a;
+  int la;
+  int rc = conv_fwd_args(DT_BF16, x8, ldx, N, H, W, Cin, w8, Cout, KH, KW, stride, pad, dil, bias, y,
+                         ldy, OH, OW, a, la);
+  if (rc) return rc;
+  a.scale_a = x_state;   // state[0] = dequantisation scale
+  a.scale_b = w_state;
+  return cn_gemm_dispatch(a, DT_FP8, 0, la, L_KC_DENSE, 1, st);
+}
+
 static long long mtiles_of(int dtype, int M, int N, int K) {
   const int bm = cn_gemm_bm(dtype, M, N, K, -1);
   return (M + bm - 1) / bm;

@@ -35,6 +35,8 @@ struct GemmArgs {
                                // 3 split-K slab store (C + split * slab)
   long long slab;              // elements between split-K slabs (c_mode 3)
   float alpha;
+  const float* scale_a;        // fp8 operands: device per-tensor dequantisation scales (C *= sa * sb)
+  const float* scale_b;
   int cfg;                     // tile configuration (gemm.hip kCfg), -1 = shape heuristic
   // BatchNorm epilogues (batch == 1, nsplit == 1, row_map == 0, c_mode 0 only):
   //  st_mode 1: per-(M-tile, column) statistics of the STORED C for train-mode BN: planes

@@ -223,6 +223,18 @@ __device__ __forceinline__ bf16x8 read_frag_bf16(const char* lds, int rowbase, i
   }
 }
 
+// fp8 (KC only): one 16x16x128 MFMA per 128-byte K tile; lane l supplies row/col (l & 15) and the
+// 32 bytes of chunks 2g, 2g+1 (g = l >> 4).  The hardware's k order within the operand is the
+// same for A and B, so reading both operands at the same byte offsets sums the right products.
+__device__ __forceinline__ i32x8 read_frag_f8(const char* lds, int rowbase, int lane) {
+  const int row = rowbase + (lane & 15), g = lane >> 4;
+  const u32x4 lo = *(const u32x4*)(lds + row * 128 + (((2 * g) ^ (row & 7)) << 4));
+  const u32x4 hi = *(const u32x4*)(lds + row * 128 + (((2 * g + 1) ^ (row & 7)) << 4));
+  i32x8 r;
+  r[0] = lo.x; r[1] = lo.y; r[2] = lo.z; r[3] = lo.w; r[4] = hi.x; r[5] = hi.y; r[6] = hi.z; r[7] = hi.w;
+  return r;
+}
+
 // fp32: piece p, step j -> k = 16p + 4(l>>4) + j ; returns the 4 floats of (p) for KC,
 // or the scalar for MC (per j).
 template <int ROWS>
@@ -370,6 +382,20 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   auto mma_tile = [&](const char* As, const char* Bs) {
+    if constexpr (sizeof(T) == 1) {
+      static_assert(!AMC && !BMC, "fp8 operands are k-contiguous (KC) only");
+      i32x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[i] = read_frag_f8(As, wm * TM + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bfr[j] = read_frag_f8(Bs, wn * TN + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)  // e4m3 x e4m3, unit block scales (E8M0 127 = 2^0)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+      return;
+    }
 #pragma unroll
     for (int pc = 0; pc < 2; ++pc) {
       if constexpr (sizeof(T) == 2) {
@@ -389,7 +415,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
 #if CN_GEMM_PRIO == 1
         __builtin_amdgcn_s_setprio(0);
 #endif
-      } else {
+      } else if constexpr (sizeof(T) == 4) {
         f32x4 af[RM], bfr[RN];
         if (!AMC) {
 #pragma unroll
@@ -482,6 +508,9 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
                    : ((BM / 4) * LDC * 4 <= S * STAGE) ? BM / 4 : BM / 8;
   static_assert(HR % 16 == 0 && HR * LDC * 4 <= S * STAGE, "epilogue staging must fit in the LDS image");
   float* cs = (float*)smem;
+  float alpha = p.alpha;
+  if (p.scale_a) alpha *= *p.scale_a;
+  if (p.scale_b) alpha *= *p.scale_b;
   CT* Cb = (CT*)p.C + (long long)batch * p.c_bs + (p.c_mode == 3 ? (long long)split * p.slab : 0);
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
   constexpr int GPR = BN / 8;            // 8-column groups per row
@@ -538,7 +567,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
         for (int j = 0; j < RN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            cs[(rb + 4 * g + r) * LDC + wn * TN + j * 16 + (lane & 15)] = acc[i][j][r] * p.alpha;
+            cs[(rb + 4 * g + r) * LDC + wn * TN + j * 16 + (lane & 15)] = acc[i][j][r] * alpha;
       }
     }
     __syncthreads();
@@ -803,8 +832,23 @@ static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_
   return -10;  // unsupported loader combination
 }
 
+// fp8 (e4m3) operands: k-contiguous loaders only (conv forward / dgrad / dense products), the
+// three tiles the shape heuristic uses; 128 fp8 per 128-byte K tile, one scaled MFMA per tile.
+template <class CT, int LA>
+static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
+  // (the 256x256 tile would spill its fp8 fragments: 128x128 serves the wide products too)
+  if (pick_cfg(a, batch) == 12) return launch_c<f8e4m3, CT, 12, LA, L_KC_DENSE>(a, batch, st);
+  return launch_c<f8e4m3, CT, 11, LA, L_KC_DENSE>(a, batch, st);
+}
+
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
+  if (dtype == DT_FP8) {
+    if (lb != L_KC_DENSE || a.st_mode || a.nsplit != 1) return CN_ERR_UNSUPPORTED;
+    if (la == L_KC_DENSE) return c_f32 ? launch_f8<float, L_KC_DENSE>(a, batch, st) : launch_f8<bf16, L_KC_DENSE>(a, batch, st);
+    if (la == L_KC_CONV) return c_f32 ? launch_f8<float, L_KC_CONV>(a, batch, st) : launch_f8<bf16, L_KC_CONV>(a, batch, st);
+    return CN_ERR_UNSUPPORTED;
+  }
   if (a.st_mode) {
     if (batch != 1 || a.nsplit != 1 || a.row_map || a.c_mode ||
         lb != L_KC_DENSE || (la != L_KC_DENSE && la != L_KC_CONV))

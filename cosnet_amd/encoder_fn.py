@@ -16,6 +16,7 @@ import torch
 
 from . import _native as nv
 from . import ops
+from .fp8 import fp8_ok
 from .ops import WCACHE, as_param_grad, bn_apply, bn_bwd, bn_stats, conv_dgrad, conv_fwd, conv_wgrad
 
 from .functions import F, _GRAD
@@ -55,10 +56,18 @@ def fuse_bwd(cin, kdim):
     return kdim >= 1024 and cin <= 256
 
 
-def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=None):
+def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=None, weight=None):
     """conv -> raw output c and the BN statistics of c per segment.  Train mode: the statistics
     come out of the conv's GEMM epilogue where that is cheaper (ops.conv_fwd_bn, no pass over c),
-    else a separate statistics pass; eval: running statistics."""
+    else a separate statistics pass; eval: running statistics.  fp8 mode (configs[4]): the
+    conv GEMM takes e4m3 operands (cosnet_amd/fp8.py), statistics by the separate pass."""
+    cin = wf.shape[1] // (k * k)
+    ctx = getattr(bn, "_cn_fp8", None)
+    if weight is not None and ctx is not None and fp8_ok(x, cin) and x.shape[0] > 64:
+        x8, xs = ctx.acts.quant(x, id(weight))
+        wf8, ws = ctx.weights.get(weight)
+        c, oh, ow = ops.conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, xs, ws, bias=bias)
+        return c, oh, ow, seg_stats(c, bn, training, nseg)
     if training and fuse_stats(cout, wf.shape[1]):
         c, oh, ow, st = ops.conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg, bias=bias)
         return c, oh, ow, SegStats(st, nseg, cout)
@@ -66,10 +75,26 @@ def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=
     return c, oh, ow, seg_stats(c, bn, training, nseg)
 
 
-def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None):
-    return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
-                    rstats=None if rstats is None else (rstats.mean, rstats.invstd), rbn=rbn,
-                    out=out, nseg=stats.nseg)
+def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None,
+              fp8_key=None):
+    """BN apply; in fp8 mode with fp8_key (the output feeds fp8 convs) also the e4m3 copy of the
+    output in the same pass (delayed scaling; a first use calibrates by a separate pass)."""
+    rs = None if rstats is None else (rstats.mean, rstats.invstd)
+    ctx = getattr(bn, "_cn_fp8", None)
+    if fp8_key is None or ctx is None or x.dtype != torch.bfloat16:
+        return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
+                        rstats=rs, rbn=rbn, out=out, nseg=stats.nseg)
+    st = ctx.acts.ready(fp8_key, x.device)
+    if st is None:
+        y = bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
+                     rstats=rs, rbn=rbn, out=out, nseg=stats.nseg)
+        ctx.acts.quant(y, fp8_key)
+        return y
+    y8 = torch.empty(tuple(x.shape), dtype=torch.uint8, device=x.device)
+    y = bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr, rstats=rs,
+                 rbn=rbn, out=out, nseg=stats.nseg, out8=y8, qstate=st)
+    ctx.acts.register(y, y8, st)
+    return y
 
 
 # ---- stem --------------------------------------------------------------------------------------
@@ -127,19 +152,23 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     w1f, w1t = WCACHE.get(blk.conv1.weight, dt)
     w2f, w2t = WCACHE.get(blk.conv2.weight, dt)
     w3f, w3t = WCACHE.get(blk.conv3.weight, dt)
-    c1, oh, ow, st1 = conv_bn(x, n, h, w, w1f, planes, 1, s, 0, 1, blk.bn1, tr, nseg)
-    y1 = seg_apply(c1, st1, blk.bn1, act=1)
-    c2, _, _, st2 = conv_bn(y1, n, oh, ow, w2f, planes, 3, 1, d, d, blk.bn2, tr, nseg)
-    y2 = seg_apply(c2, st2, blk.bn2, act=1)
-    c3, _, _, st3 = conv_bn(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1, blk.bn3, tr, nseg)
+    c1, oh, ow, st1 = conv_bn(x, n, h, w, w1f, planes, 1, s, 0, 1, blk.bn1, tr, nseg,
+                              weight=blk.conv1.weight)
+    y1 = seg_apply(c1, st1, blk.bn1, act=1, fp8_key=id(blk.conv2.weight))
+    c2, _, _, st2 = conv_bn(y1, n, oh, ow, w2f, planes, 3, 1, d, d, blk.bn2, tr, nseg,
+                            weight=blk.conv2.weight)
+    y2 = seg_apply(c2, st2, blk.bn2, act=1, fp8_key=id(blk.conv3.weight))
+    c3, _, _, st3 = conv_bn(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1, blk.bn3, tr, nseg,
+                            weight=blk.conv3.weight)
     cd = std = wdt = None
     if blk.downsample is not None:
         wdf, wdt = WCACHE.get(blk.downsample[0].weight, dt)
         bnd = blk.downsample[1]
-        cd, _, _, std = conv_bn(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1, bnd, tr, nseg)
-        y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd)
+        cd, _, _, std = conv_bn(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1, bnd, tr, nseg,
+                                weight=blk.downsample[0].weight)
+        y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd, fp8_key=("out", id(blk)))
     else:
-        y = seg_apply(c3, st3, blk.bn3, act=1, res=x)
+        y = seg_apply(c3, st3, blk.bn3, act=1, res=x, fp8_key=("out", id(blk)))
     if rec is not None:
         rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt),
                     (n // nseg, h, w, oh, ow, s, d, planes, x.shape[1])))
@@ -199,19 +228,39 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     yp = seg_apply(cp, stp, mod.bn_x, act=1)
     nv.call("cn_bcast_rows", ops.dtc(yp), yp.data_ptr(), n, hw, 512, 1.0, cat.data_ptr(), 2560, 0,
             nv.stream())
+    # fp8 mode: the concat's e4m3 copy for the bottleneck conv, written by the branches' applies
+    # (one delayed-scaling state for the whole concat; the pooled slice by a quantise pass)
+    cat8 = qst = None
+    ctx = getattr(mod, "_cn_fp8", None) if dt == torch.bfloat16 else None
+    if ctx is not None:
+        qst = ctx.acts.ready(("cat", id(mod)), dev)
+        if qst is not None:
+            cat8 = torch.empty((P, 2560), dtype=torch.uint8, device=dev)
+            ops.fp8_quant(cat[:, :512], qst, ops.FP8_DELAYED, out=cat8[:, :512])
     convs = [(mod.conv2d_0, mod.bn_0, 1, 0)] + [
         (getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)), 3, dd)
         for i, dd in enumerate(mod.cn_dilations)]
     cs, sts, wts = [], [], []
     for bi, (cm, bnm, k, dd) in enumerate(convs):
         wf, wt = WCACHE.get(cm.weight, dt)
-        ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias)
-        seg_apply(ci, st, bnm, act=1, out=cat[:, 512 * (bi + 1):512 * (bi + 2)])
+        ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias,
+                               weight=cm.weight)
+        sl = slice(512 * (bi + 1), 512 * (bi + 2))
+        if cat8 is not None:
+            bn_apply(ci, (st.mean, st.invstd), bnm, act=1, out=cat[:, sl], nseg=st.nseg,
+                     out8=cat8[:, sl], qstate=qst)
+        else:
+            seg_apply(ci, st, bnm, act=1, out=cat[:, sl])
         cs.append(ci)
         sts.append(st)
         wts.append(wt)
+    if cat8 is not None:
+        ctx.acts.register(cat, cat8, qst)
+    elif ctx is not None:
+        ctx.acts.quant(cat, ("cat", id(mod)))   # first use: calibrates the concat's scale
     wbf, wbt = WCACHE.get(mod.bottleneck.weight, dt)
-    cb, _, _, stb = conv_bn(cat, n, h, w, wbf, 256, 3, 1, 1, 1, mod.bn, tr, nseg, bias=mod.bottleneck.bias)
+    cb, _, _, stb = conv_bn(cat, n, h, w, wbf, 256, 3, 1, 1, 1, mod.bn, tr, nseg, bias=mod.bottleneck.bias,
+                            weight=mod.bottleneck.weight)
     out = seg_apply(cb, stb, mod.bn, act=2, prelu=mod.prelu.weight)
     if rec is not None:
         rec.append(("aspp", mod, (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out),
@@ -266,13 +315,18 @@ class EncoderPairFn(F):
     @staticmethod
     def forward(ctx, img_a, img_b, enc, *params):
         dt = getattr(enc, "_cn_dtype", torch.bfloat16)
+        fp8 = getattr(enc, "_cn_fp8", None)
         rec = [] if (_GRAD[0] and any(ctx.needs_input_grad[3:])) else None
         nseg = 2
+        if fp8 is not None:
+            fp8.acts.begin()
         x, geo = stem_fwd(enc.backbone, (img_a, img_b), nseg, dt, rec)
         for layer in (enc.backbone.layer1, enc.backbone.layer2, enc.backbone.layer3, enc.backbone.layer4):
             for blk in layer:
                 x, geo = bottleneck_fwd(blk, x, geo, nseg, rec)
         out = aspp_fwd(enc.aspp, x, geo, nseg, rec)
+        if fp8 is not None:
+            fp8.acts.end()
         half = out.shape[0] // 2
         ctx.rec = rec
         ctx.params = params

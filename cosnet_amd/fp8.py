@@ -1,0 +1,166 @@
+"""fp8 (OCP e4m3) forward convolutions: BASELINE configs[4] ("fp8 MFMA ... implicit-GEMM conv").
+
+Recipe (the usual fp8-training split): the encoder convs' FORWARD GEMMs take e4m3 operands
+with per-tensor scales on the block-scaled MFMA (cn_conv_fwd_fp8, 2x the bf16 MFMA rate);
+everything else -- BatchNorm, activations, the co-attention, the whole backward (which reads
+the bf16 activations saved by the forward), the fp32 master weights and SGD -- stays as in the
+bf16 path.
+
+* Weights: current scaling.  Each conv weight has an fp8 copy [Cout][KH*KW*Cin] and a scale
+  state; after every SGD step all copies are re-quantised from the fp32 masters in three
+  launches (cn_fp8_quant_multi: amax, scale, quantise), inside the recorded step graph.
+* Activations: delayed scaling.  A conv input is quantised once per forward (shared by the
+  convs that read it) with the scale derived from the previous step's amax of that tensor,
+  while this step's amax is collected; one cn_fp8_update per encoder pass advances all scales.
+  A state is calibrated (amax pass) on first use, so step 0 does not saturate.
+"""
+import struct
+import weakref
+
+import numpy as np
+import torch
+
+from . import _native as nv
+from . import ops
+
+_REC = struct.Struct("<QqiiQqQq")   # Fp8Rec (fp8.hip): x, ldx, P, C, y, ldy, state, pad
+assert _REC.size == 56
+
+
+def fp8_ok(x, cin):
+    return x.dtype == torch.bfloat16 and cin % 16 == 0 and ops.ld(x) % 16 == 0
+
+
+class Fp8Weights:
+    """fp8 copies of fp32 conv weights (channels_last), refreshed after each optimiser step."""
+
+    def __init__(self):
+        self._c = {}          # id(w) -> [wf8, state, tag, weakref]
+        self._table = None
+        self._table_n = 0
+
+    @staticmethod
+    def _tag(w):
+        return (w._version, w.data_ptr())
+
+    def get(self, w):
+        e = self._c.get(id(w))
+        if e is None:
+            cout = w.shape[0]
+            k = w.numel() // cout
+            wf8 = torch.empty((cout, k), dtype=torch.uint8, device=w.device)
+            e = [wf8, ops.fp8_state(w.device), None, w]
+            self._c[id(w)] = e
+            self._table = None
+        if e[2] != self._tag(w):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fp8 weight copy is stale inside a graph capture")
+            cin = w.shape[1]
+            nv.call("cn_fp8_quant", nv.DT_F32, w.data_ptr(), cin, w.numel() // cin, cin,
+                    e[0].data_ptr(), cin, e[1].data_ptr(), ops.FP8_CURRENT, nv.stream())
+            e[2] = self._tag(w)
+        return e[0], e[1]
+
+    def refresh_all(self):
+        """Re-quantise every fp8 copy from its (just updated) master: 3 launches."""
+        if not self._c:
+            return
+        if self._table is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fp8 weight table must be built before graph capture")
+            blob = b""
+            for wf8, st, _, w in self._c.values():
+                cin = w.shape[1]
+                blob += _REC.pack(w.data_ptr(), cin, w.numel() // cin, cin, wf8.data_ptr(), cin,
+                                  st.data_ptr(), 0)
+            host = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy())
+            dev = next(iter(self._c.values()))[0].device
+            self._table = host.to(dev)
+            self._table_n = len(self._c)
+        nv.call("cn_fp8_quant_multi", self._table.data_ptr(), self._table_n, nv.stream())
+        for e in self._c.values():
+            e[2] = self._tag(e[3]) if e[3] is not None else None
+
+    def mark_updated(self):
+        """The masters changed in place (SGD): copies valid after refresh_all()."""
+        for e in self._c.values():
+            e[2] = self._tag(e[3])
+
+
+class Fp8Acts:
+    """Delayed-scaling states of the conv inputs, in one device buffer (one update launch)."""
+
+    def __init__(self, cap=1024):
+        self.cap = cap
+        self.states = None
+        self.slots = {}
+        self.calibrated = set()
+        self.pass_cache = {}
+
+    def begin(self):
+        self.pass_cache = {}
+
+    def state(self, key, device):
+        if self.states is None:
+            self.states = torch.tensor([[1.0, 1.0, 0.0, 0.0]] * self.cap, dtype=torch.float32,
+                                       device=device)
+        i = self.slots.get(key)
+        if i is None:
+            i = len(self.slots)
+            if i >= self.cap:
+                raise RuntimeError("too many fp8 activation states")
+            self.slots[key] = i
+        return i, self.states[i]
+
+    def quant(self, x, key):
+        """x8 of x (bf16 [P, C]) under this key's delayed scale; cached for the pass."""
+        ck = (x.data_ptr(), tuple(x.shape), ops.ld(x))
+        hit = self.pass_cache.get(ck)
+        if hit is not None:
+            return hit[0], hit[1]
+        i, st = self.state(key, x.device)
+        if i not in self.calibrated:   # first use: this tensor's own amax sets the scale
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fp8 activation state first used inside a graph capture")
+            ops.fp8_quant(x, st, ops.FP8_AMAX)
+            ops.fp8_update(st)
+            self.calibrated.add(i)
+        x8 = ops.fp8_quant(x, st, ops.FP8_DELAYED)
+        self.pass_cache[ck] = (x8, st, x)   # x held: its address cannot be reused this pass
+        return x8, st
+
+    def ready(self, key, device):
+        """(slot state) if this key's scale is calibrated (a producer may quantise in its own
+        pass), else None."""
+        i, st = self.state(key, device)
+        return st if i in self.calibrated else None
+
+    def register(self, x, x8, st):
+        """x8 / st are the fp8 copy of x produced elsewhere (bn_apply's fused output)."""
+        self.pass_cache[(x.data_ptr(), tuple(x.shape), ops.ld(x))] = (x8, st, x)
+
+    def end(self):
+        """Advance every used scale from the amax collected in this pass (one launch)."""
+        self.pass_cache = {}
+        if self.slots:
+            ops.fp8_update(self.states[:len(self.slots)])
+
+
+class Fp8Context:
+    """One model's fp8 state: weight copies + activation scales (model.set_fp8 creates it; the
+    modules reach it through their `_cn_fp8` attribute).  Per model, so that a state is never
+    picked up by another model whose modules happen to reuse a freed object's id."""
+
+    def __init__(self):
+        self.weights = Fp8Weights()
+        self.acts = Fp8Acts()
+        LIVE.add(self)
+
+
+LIVE = weakref.WeakSet()
+
+
+def refresh_all_weights():
+    """After an optimiser step: re-quantise every live context's fp8 weight copies."""
+    for ctx in list(LIVE):
+        ctx.weights.refresh_all()

@@ -246,6 +246,46 @@ def bn_bwd_apply(x, dy, stats, bn, dgamma, dbeta, out=None):
     return out
 
 
+# ---- fp8 (e4m3) operands (BASELINE configs[4]) ------------------------------------------------
+def fp8_state(device):
+    """Per-tensor fp8 scaling state [scale, 1/scale, amax, -] (cn_fp8_quant)."""
+    return torch.tensor([1.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=device)
+
+
+FP8_DELAYED, FP8_CURRENT, FP8_AMAX = 0, 1, 2
+
+
+def fp8_quant(x, state, mode=FP8_CURRENT, out=None):
+    """x [P, C] (fp32 / bf16) -> e4m3 bytes [P, C] (uint8) scaled by state (see fp8_state)."""
+    p, c = x.shape
+    if out is None and mode != FP8_AMAX:
+        out = torch.empty((p, c), dtype=torch.uint8, device=x.device)
+    nv.call("cn_fp8_quant", dtc(x), x.data_ptr(), ld(x), p, c, nv.ptr(out),
+            ld(out) if out is not None else c, state.data_ptr(), mode, nv.stream())
+    return out
+
+
+def fp8_update(states, margin=1.0):
+    """Turn each state's collected amax into its next scale (states: [n, 4] or [4])."""
+    nv.call("cn_fp8_update", states.data_ptr(), states.numel() // 4, float(margin), nv.stream())
+
+
+def conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, bias=None,
+                 out=None):
+    """y (bf16) = conv(x8, w8) * sx * sw (+ bias): the fp8 implicit-GEMM conv."""
+    cin = wf8.shape[1] // (k * k)
+    oh, ow = out_hw(h, w, k, stride, pad, dil)
+    if out is None:
+        out = torch.empty((n * oh * ow, cout), dtype=torch.bfloat16, device=x8.device)
+    ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("fwd8", n * oh * ow, cout, k * k * cin),
+                     n * h * w * cin + cout * k * k * cin + 2 * n * oh * ow * cout)
+    nv.call("cn_conv_fwd_fp8", x8.data_ptr(), ld(x8), n, h, w, cin, wf8.data_ptr(), cout, k, k,
+            stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, x_state.data_ptr(),
+            w_state.data_ptr(), nv.stream())
+    _prof_end(ev)
+    return out, oh, ow
+
+
 def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accumulate=False):
     cout = wt.shape[1] // (k * k)
     if out is None:
@@ -481,18 +521,20 @@ def _affine(bn):
 
 
 def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None,
-             nseg=1):
-    """y = act(bn(x) [+ res] [+ rbn(xr)]) with per-segment statistics ([nseg*C] each)."""
+             nseg=1, out8=None, qstate=None):
+    """y = act(bn(x) [+ res] [+ rbn(xr)]) with per-segment statistics ([nseg*C] each); with
+    out8 / qstate also an fp8 copy of y (delayed scaling, amax collected into qstate)."""
     p, c = x.shape
     if out is None:
         out = torch.empty((p, c), dtype=x.dtype, device=x.device)
     g, b = _affine(bn)
     rg, rb = _affine(rbn) if rbn is not None else (None, None)
-    nv.call("cn_bn_apply", dtc(x), x.data_ptr(), ld(x), p // nseg, nseg, c, stats[0].data_ptr(),
+    nv.call("cn_bn_apply_fp8", dtc(x), x.data_ptr(), ld(x), p // nseg, nseg, c, stats[0].data_ptr(),
             stats[1].data_ptr(), nv.ptr(g), nv.ptr(b), nv.ptr(res), ld(res) if res is not None else 0,
             nv.ptr(xr), ld(xr) if xr is not None else 0, nv.ptr(rstats[0] if rstats else None),
             nv.ptr(rstats[1] if rstats else None), nv.ptr(rg), nv.ptr(rb), act, nv.ptr(prelu),
-            out.data_ptr(), ld(out), nv.stream())
+            out.data_ptr(), ld(out), nv.ptr(out8), ld(out8) if out8 is not None else 0,
+            nv.ptr(qstate), nv.stream())
     return out
 
 

@@ -204,6 +204,9 @@ class SGD:
         # one: those cache entries stay valid (no re-preparation before the next forward)
         for ent in refreshed:
             WCACHE.refreshed(ent)
+        # fp8 copies (configs[4]): re-quantised from the new masters, 3 launches for all
+        from .fp8 import refresh_all_weights
+        refresh_all_weights()
 
     def _upload_lrs(self, dev):
         if self._lr_dev is None:

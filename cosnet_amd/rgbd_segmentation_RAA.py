@@ -55,6 +55,7 @@ class RGBDSegmentation_RAA(nn.Module):
         if num_classes != 1:
             raise ValueError("the HIP decoder head is built for num_classes=1 (train.py:379)")
         self.compute_dtype = torch.bfloat16
+        self.fp8 = None            # Fp8Context: e4m3 forward conv GEMMs in the encoders (configs[4])
         self.pair_encoder = True   # batch frames a and b through each encoder (encoder_fn.py)
         self._to_channels_last()
         self.register_state_dict_pre_hook(_flush_bn_counters)
@@ -136,9 +137,19 @@ class RGBDSegmentation_RAA(nn.Module):
             raise RuntimeError("RGBDSegmentation_RAA (HIP) expects inputs on the GPU")
         return t.float().contiguous()
 
+    def set_fp8(self, on=True):
+        """fp8 (OCP e4m3) operands for the encoders' forward conv GEMMs (cosnet_amd/fp8.py);
+        needs the bf16 compute dtype."""
+        if on and self.compute_dtype != torch.bfloat16:
+            raise ValueError("fp8 convs run inside the bf16 path")
+        from .fp8 import Fp8Context
+        self.fp8 = Fp8Context() if on else None
+        return self
+
     def _set_dtype(self):
         for m in self.modules():
             m._cn_dtype = self.compute_dtype
+            m._cn_fp8 = self.fp8
 
     def forward(self, rgbs_a, rgbs_b, depths_a, depths_b, stages=None):
         self._set_dtype()

@@ -5,7 +5,8 @@
  * Conventions
  *   - activations are NHWC "pixel-major" matrices [P][C] with a row stride ld (elements);
  *     a channel slice of a concat buffer is (base + offset, ld)
- *   - dtype: 0 = fp32 (parity path), 1 = bf16 (throughput path); accumulation is fp32
+ *   - dtype: 0 = fp32 (parity path), 1 = bf16 (throughput path), 2 = fp8 e4m3 (OCP, matrix
+ *     operands only: cn_fp8_quant / cn_conv_fwd_fp8); accumulation is fp32
  *   - conv weights are [Cout][KH][KW][Cin] (= torch channels_last of [Cout,Cin,KH,KW]);
  *     dgrad takes the transposed copy [Cin][KH][KW][Cout] (cn_weight_prep makes both)
  *   - all buffers are caller-owned device memory (the library never allocates); the
@@ -54,6 +55,26 @@ int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, 
 /* out[i] (+)= sum_s ws[s*slab + i], s < nsplit  (split-K reduction, fp32) */
 int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                      int accumulate, hipStream_t stream);
+
+/* ---- fp8 (e4m3, OCP) operands: BASELINE configs[4] -------------------------------------- */
+/* Per-tensor scaling state (4 floats, caller-owned, init {1, 1, 0, 0}): [0] dequantisation scale,
+ * [1] its inverse, [2] running amax.  mode 0 (delayed scaling): y8 = fp8(x * state[1]) and amax
+ * collected; mode 1 (current scaling): amax pass, update, quantise; mode 2: amax only.
+ * x: [P][C] (ldx) fp32 or bf16, C % 8 == 0; y8: [P][C] bytes (ldy). */
+int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int C, void* y8, long long ldy,
+                 float* state, int mode, hipStream_t stream);
+/* Current scaling of n fp32 matrices in three launches (amax, update, quantise): device table
+ * of n records {const float* x; long long ldx; int P, C; uint8* y; long long ldy; float* state;
+ * long long pad} (56 bytes each) -- the fp8 copies of the conv weights after each SGD step. */
+int cn_fp8_quant_multi(const void* recs, int n, hipStream_t stream);
+/* scale = amax * margin / 448 for each of nstates consecutive states; amax reset */
+int cn_fp8_update(float* states, int nstates, float margin, hipStream_t stream);
+/* y (bf16) = conv2d(x8, w8) * x_state[0] * w_state[0] + bias: the fp8 implicit-GEMM conv
+ * (block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales).  Cin % 16 == 0. */
+int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin, const void* w8,
+                    int Cout, int KH, int KW, int stride, int pad, int dil, const float* bias,
+                    void* y, long long ldy, int OH, int OW, const float* x_state,
+                    const float* w_state, hipStream_t stream);
 
 /* Conv + train-mode BatchNorm statistics in ONE pass: y = conv2d(x, w) + bias as cn_conv_fwd,
  * and the GEMM epilogue reduces per-tile column partials of the stored y, so no separate pass
@@ -108,6 +129,15 @@ int cn_bn_apply(int dtype, const void* x, long long ldx, int P, int nseg, int C,
                 const void* res, long long ldr, const void* xr, long long ldxr,
                 const float* rmean, const float* rinvstd, const float* rgamma, const float* rbeta,
                 int act, const float* prelu, void* y, long long ldy, hipStream_t stream);
+/* cn_bn_apply that also writes y8 = fp8(y * qstate[1]) (bf16 only) and collects amax|y| into
+ * qstate[2] (cn_fp8_quant's delayed scaling): the producer of an fp8 conv's input quantises it
+ * in the same pass. */
+int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                    const float* mean, const float* invstd, const float* gamma, const float* beta,
+                    const void* res, long long ldr, const void* xr, long long ldxr,
+                    const float* rmean, const float* rinvstd, const float* rgamma,
+                    const float* rbeta, int act, const float* prelu, void* y, long long ldy,
+                    void* y8, long long ldy8, float* qstate, hipStream_t stream);
 /* launch-shape knobs (blocks / rows per thread of each BN pass), for tuning only */
 int cn_bn_set_tuning(int key, int value);
 /* backward of cn_bn_apply w.r.t. x (train mode), masks fused; dres <- dz for the residual */

@@ -608,3 +608,58 @@ def test_conv_dgrad_bn_epilogue_reduce(cuda, dt, case):
         for got, ref in ((dbet, bet.grad), (nchw(dx, n, h, w), xr.grad)):
             got, ref = got.double().cpu(), ref.double()
             assert (got - ref).abs().mean().item() <= 2e-2 * ref.abs().mean().item()
+
+
+def _dec_e4m3(u8):
+    """Exact decode of OCP e4m3fn bytes (torch's float8_e4m3fn view)."""
+    return u8.cpu().view(torch.float8_e4m3fn).double()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fp8_quant_matches_torch_e4m3fn(cuda, dt):
+    """cn_fp8_quant (current scaling): scale = amax / 448, bytes = e4m3fn(x / scale) saturating,
+    against torch's float8_e4m3fn conversion (round to nearest even)."""
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn((300, 96), generator=g) * 3.0).to(dt)
+    st = ops.fp8_state(cuda)
+    y8 = ops.fp8_quant(x.to(cuda), st, ops.FP8_CURRENT)
+    torch.cuda.synchronize()
+    amax = x.double().abs().max().item()
+    assert abs(st[0].item() - amax / 448) <= 1e-6 * amax
+    ref = (x.double() * st[1].double().cpu()).clamp(-448, 448).to(torch.float8_e4m3fn)
+    got = _dec_e4m3(y8)
+    diff = (got - ref.double()).abs()
+    ulp = ref.double().abs().clamp_min(2 ** -6) * 2 ** -3   # one e4m3 mantissa step
+    assert (diff <= ulp * 1.001).all()
+    assert (diff == 0).double().mean().item() >= 0.999     # ties only may differ
+    # delayed scaling: quantise with the stored scale, collect the amax, update
+    y2 = ops.fp8_quant((x * 2).to(cuda), st, ops.FP8_DELAYED)
+    ops.fp8_update(st)
+    torch.cuda.synchronize()
+    assert _dec_e4m3(y2).abs().max().item() == 448.0            # saturated at the old scale
+    assert abs(st[0].item() - 2 * amax / 448) <= 1e-6 * amax      # next scale from the new amax
+
+
+@pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 1, 0, 1), (2, 32, 15, 9, 64, 3, 1, 2, 2),
+                                  (1, 256, 12, 12, 256, 3, 1, 1, 1), (2, 256, 7, 9, 128, 1, 2, 0, 1),
+                                  (4, 128, 30, 30, 512, 3, 1, 4, 4)])
+def test_conv_fwd_fp8(cuda, case):
+    """cn_conv_fwd_fp8 against fp64 conv2d of the exactly-decoded fp8 operands times their
+    scales: checks the block-scaled MFMA's operand lane map (asymmetric data) and the
+    dequantisation; only fp32 accumulation and the bf16 output rounding remain (1e-2)."""
+    n, cin, h, w, cout, k, s, p, d = case
+    x = rnd((n, cin, h, w), torch.float32, 31, scale=2.0)
+    wt = rnd((cout, cin, k, k), torch.float32, 32, scale=(2.0 / (cin * k * k)) ** 0.5)
+    xs, ws = ops.fp8_state(cuda), ops.fp8_state(cuda)
+    x8 = ops.fp8_quant(nhwc(x).float().to(cuda).contiguous(), xs, ops.FP8_CURRENT)
+    w8 = ops.fp8_quant(wt.permute(0, 2, 3, 1).reshape(cout * k * k, cin).float().to(cuda).contiguous(),
+                       ws, ops.FP8_CURRENT).view(cout, k * k * cin)
+    bias = rnd((cout,), torch.float32, 33).float().to(cuda)
+    y, oh, ow = ops.conv_fwd_fp8(x8, n, h, w, w8, cout, k, s, p, d, xs, ws, bias=bias)
+    torch.cuda.synchronize()
+    xq = nchw(_dec_e4m3(x8), n, h, w) * xs[0].double().cpu()
+    wq = _dec_e4m3(w8).reshape(cout, k, k, cin).permute(0, 3, 1, 2) * ws[0].double().cpu()
+    ref = F.conv2d(xq, wq, bias.double().cpu(), s, p, d)
+    got = nchw(y, n, oh, ow).double().cpu()
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 1e-2, err
