@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
+    ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="data-parallel gradient buckets reduced in fp32 (default) or bf16")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path on one device (not a measurement)")
     return ap.parse_args()
 
 
@@ -171,10 +175,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":   # rehearsal: every rank on device 0
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     import cosnet_amd as C
@@ -197,7 +206,7 @@ def main():
     opt = SGD([g0, g1], [0.0, 0.0], momentum=0.9, weight_decay=5e-4)
 
     B, S = args.batch, args.size
-    step = TrainStep(model, opt, B, S, graphed=bool(args.graph))
+    step = TrainStep(model, opt, B, S, graphed=bool(args.graph), grad_dtype=args.grad_dtype)
     step.load(*[t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)])
     max_iter = 10000
 
@@ -259,6 +268,8 @@ def main():
                                "batch %d pairs/GPU" % (S, S, B),
                    "model": "RGBDSegmentation_RAA(Bottleneck,[3,4,23,3],[3,4,6,3],1)",
                    "global_batch": B * world, "image_hw": [S, S], "parallelism": "dp%d" % world,
+                   "grad_reduce": "%s buckets overlapped with the encoder backward" % args.grad_dtype
+                   if world > 1 else None,
                    "loss": float(loss.item())},
         "model_tflops_per_s": pairs * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
     }

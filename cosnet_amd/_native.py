@@ -72,6 +72,7 @@ _SIGS = {
     "cn_mean_rows": (_I, [_P, _I, _I, _P, _P]),
     "cn_sum_rows": (_I, [_P, _I, _I, _P, _P]),
     "cn_scale_dev": (_I, [_P, _L, _P, _P, _P]),
+    "cn_scale": (_I, [_P, _L, _F, _P]),
     "cn_soft_iou": (_I, [_P, _P, _I, _L, _P, _P, _P, _P]),
     "cn_frame_resize": (_I, [_I, _P, _I, _L, _L, _L, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P]),
     "cn_gemm_force_config": (_I, [_I]),

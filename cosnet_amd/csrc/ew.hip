@@ -881,6 +881,19 @@ __global__ void scale_dev_k(const float* __restrict__ x, long long n, const floa
     out[i] = x[i] * f;
 }
 
+__global__ void scale_k(float* __restrict__ x, long long n, float s) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    x[i] *= s;
+}
+
+extern "C" int cn_scale(float* x, long long n, float s, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(scale_k, dim3(nblocks(n)), dim3(256), 0, st, x, n, s);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int cn_scale_dev(const float* x, long long n, const float* s, float* out, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(scale_dev_k, dim3(nblocks(n)), dim3(256), 0, st, x, n, s, out);

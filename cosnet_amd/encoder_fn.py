@@ -22,6 +22,31 @@ from .ops import WCACHE, as_param_grad, bn_apply, bn_bwd, bn_stats, conv_dgrad, 
 from .functions import F, _GRAD
 
 
+# ---- gradient destinations ------------------------------------------------------------------
+class GradSink(dict):
+    """Where the hand-written encoder backward puts parameter gradients.  Plain: fresh tensors
+    collected here and handed to autograd.  With a gradient arena ({param: flat fp32 slice}, the
+    data-parallel bucket buffer) every gradient is written straight into its slice: the big ones
+    by the producing kernels themselves (buf()), the rest copied in on assignment."""
+
+    def __init__(self, arena=None):
+        super().__init__()
+        self.arena = arena
+
+    def buf(self, p, *shape):
+        if self.arena is None or p not in self.arena:
+            return None
+        return self.arena[p].view(*shape)
+
+    def __setitem__(self, p, g):
+        if self.arena is not None and p in self.arena:
+            dst = self.arena[p]
+            if g.data_ptr() != dst.data_ptr():   # not produced in place (the stem's padded dw)
+                dst.as_strided(p.shape, p.stride()).copy_(g)
+            return
+        super().__setitem__(p, g)
+
+
 # ---- segment helpers -----------------------------------------------------------------------
 class SegStats:
     """BN statistics of nseg stacked frame segments: mean / invstd [nseg*C]; [i] -> segment i."""
@@ -124,21 +149,24 @@ def stem_bwd(item, dout, grads):
     dy = torch.empty((pa, 64), dtype=dout.dtype, device=dout.device)
     nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n1, oh, ow, 64, ph,
             pw, 3, 2, 1, dy.data_ptr(), nv.stream())
-    dc, dg, db, _ = bn_bwd(c[:pa], dy, None, st[0], res.bn1, act=1)
+    dc, dg, db, _ = bn_bwd(c[:pa], dy, None, st[0], res.bn1, act=1,
+                           dgamma=grads.buf(res.bn1.weight, 64), dbeta=grads.buf(res.bn1.bias, 64))
     dw = conv_wgrad(x[:n1 * h * w], n1, h, w, 8, dc, oh, ow, 64, 7, 2, 3, 1)
     grads[res.conv1.weight] = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
     grads[res.bn1.weight] = dg
     grads[res.bn1.bias] = db
 
 
-def dgrad_bn_bwd(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn):
+def dgrad_bn_bwd(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn, grads):
     """Stride-1 conv dgrad followed by the backward of the BN + ReLU (mask from x) that fed the
     conv: returns (dx of the BN input, dgamma, dbeta)."""
+    dgo, dbo = grads.buf(bn.weight, cin), grads.buf(bn.bias, cin)
     if fuse_bwd(cin, wt.shape[1]):
-        dyb, dg, db = ops.conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn)
+        dyb, dg, db = ops.conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn,
+                                        dgamma=dgo, dbeta=dbo)
         return ops.bn_bwd_apply(x, dyb, stats, bn, dg, db), dg, db
     dyb = conv_dgrad(dy, n, oh, ow, wt, cin, k, 1, pad, dil, oh, ow)
-    dx, dg, db, _ = bn_bwd(x, dyb, None, stats, bn, act=1)
+    dx, dg, db, _ = bn_bwd(x, dyb, None, stats, bn, act=1, dgamma=dgo, dbeta=dbo)
     return dx, dg, db
 
 
@@ -182,24 +210,29 @@ def bottleneck_bwd(item, dy, grads, need_dx=True):
     x, c1, y1, c2, y2, c3, y = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], y[:po]
     has_down = cd is not None
     dx = None
+    g3o, b3o = grads.buf(blk.bn3.weight, 4 * planes), grads.buf(blk.bn3.bias, 4 * planes)
     if has_down:
         cd = cd[:po]
-        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1)
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dgamma=g3o, dbeta=b3o)
         dcd, _, _, _ = bn_bwd(cd, dy, y, std[0], blk.downsample[1], act=1)
     else:
         dx = torch.empty_like(x)
-        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx)
-    dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx, dgamma=g3o, dbeta=b3o)
+    dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1,
+                     dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
     # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where
     # that is cheaper (fuse_bwd)
-    dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2)
-    dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
-    dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1)
-    dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
+    dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads)
+    dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
+                     dw=grads.buf(blk.conv2.weight, planes, 9 * planes))
+    dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1, grads)
+    dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1,
+                     dw=grads.buf(blk.conv1.weight, planes, cin))
     if need_dx:
         dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
     if has_down:
-        dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1)
+        dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1,
+                         dw=grads.buf(blk.downsample[0].weight, 4 * planes, cin))
         grads[blk.downsample[0].weight] = as_param_grad(dwd, blk.downsample[0].weight)
         if need_dx:
             conv_dgrad(dcd, n, oh, ow, wdt, cin, 1, s, 0, 1, h, w, out=dx, accumulate=True)
@@ -276,10 +309,13 @@ def aspp_bwd(item, dout, grads):
     x, cat, cb, out = x[:P], cat[:P], cb[:P], out[:P]
     pool, cp, yp = pool[:n], cp[:n], yp[:n]
     pw = mod.prelu.weight
-    dcb, dgb, dbb, dpr = bn_bwd(cb, dout, out, stb[0], mod.bn, act=2, prelu=pw)
+    dcb, dgb, dbb, dpr = bn_bwd(cb, dout, out, stb[0], mod.bn, act=2, prelu=pw,
+                                dgamma=grads.buf(mod.bn.weight, 256), dbeta=grads.buf(mod.bn.bias, 256),
+                                dprelu=grads.buf(pw, 1))
     grads[mod.bottleneck.weight] = as_param_grad(
-        conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1), mod.bottleneck.weight)
-    grads[mod.bottleneck.bias] = ops.colsum(dcb)
+        conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1,
+                   dw=grads.buf(mod.bottleneck.weight, 256, 9 * 2560)), mod.bottleneck.weight)
+    grads[mod.bottleneck.bias] = ops.colsum(dcb, out=grads.buf(mod.bottleneck.bias, 256))
     grads[mod.bn.weight], grads[mod.bn.bias], grads[pw] = dgb, dbb, dpr
     dcat = conv_dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, 1, h, w)
     dx = None
@@ -287,19 +323,23 @@ def aspp_bwd(item, dout, grads):
     cms = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
     for bi, ((k, dd), ci, st, wt) in enumerate(zip(kd, cs, sts, wts)):
         sl = slice(512 * (bi + 1), 512 * (bi + 2))
-        dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], None, st[0], bns[bi], act=1)
+        dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], None, st[0], bns[bi], act=1,
+                                  dgamma=grads.buf(bns[bi].weight, 512), dbeta=grads.buf(bns[bi].bias, 512))
         grads[cms[bi].weight] = as_param_grad(
-            conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1)), cms[bi].weight)
-        grads[cms[bi].bias] = ops.colsum(dci)
+            conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1),
+                       dw=grads.buf(cms[bi].weight, 512, k * k * 2048)), cms[bi].weight)
+        grads[cms[bi].bias] = ops.colsum(dci, out=grads.buf(cms[bi].bias, 512))
         grads[bns[bi].weight], grads[bns[bi].bias] = dgi, dbi
         dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
                         accumulate=dx is not None)
     dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
     ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
-    dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp[0], mod.bn_x, act=1)
-    grads[mod.conv.weight] = as_param_grad(conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1),
+    dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp[0], mod.bn_x, act=1,
+                              dgamma=grads.buf(mod.bn_x.weight, 512), dbeta=grads.buf(mod.bn_x.bias, 512))
+    grads[mod.conv.weight] = as_param_grad(conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1,
+                                                      dw=grads.buf(mod.conv.weight, 512, 2048)),
                                            mod.conv.weight)
-    grads[mod.conv.bias] = ops.colsum(dcp)
+    grads[mod.conv.bias] = ops.colsum(dcp, out=grads.buf(mod.conv.bias, 512))
     grads[mod.bn_x.weight], grads[mod.bn_x.bias] = dgx, dbx
     dpool = conv_dgrad(dcp, n, 1, 1, wct, 2048, 1, 1, 0, 1, 1, 1)
     nv.call("cn_bcast_rows", ops.dtc(dpool), dpool.data_ptr(), n, hw, 2048, 1.0 / hw,
@@ -331,6 +371,7 @@ class EncoderPairFn(F):
         ctx.rec = rec
         ctx.params = params
         ctx.training = enc.training
+        ctx.defer = getattr(enc, "_cn_defer", None) if rec is not None else None
         ctx.set_materialize_grads(False)
         fa, fb = out[:half], out[half:]
         ctx.mark_non_differentiable(fb)
@@ -343,13 +384,73 @@ class EncoderPairFn(F):
             return (None,) * (3 + len(ctx.params))
         if not ctx.training:
             raise RuntimeError("backward through BatchNorm is implemented for train mode only")
-        grads = {}
-        dx = aspp_bwd(rec[-1], dfa if dfa.stride(1) == 1 else dfa.contiguous(), grads)
+        dfa = dfa if dfa.stride(1) == 1 else dfa.contiguous()
+        ctx.rec = None
+        if ctx.defer is not None:
+            # data-parallel step: the encoder backward runs later, segment by segment, each
+            # segment's gradients all-reduced while the next one computes (DeferredEncoderBwd)
+            ctx.defer.stash(rec, dfa)
+            return (None,) * (3 + len(ctx.params))
+        grads = GradSink()
+        dx = aspp_bwd(rec[-1], dfa, grads)
         for item in reversed(rec[1:-1]):
             dx = bottleneck_bwd(item, dx, grads)
         stem_bwd(rec[0], dx, grads)
-        ctx.rec = None
         return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
+
+
+class DeferredEncoderBwd:
+    """The encoder backward of a data-parallel step, split into segments that write their
+    gradients straight into the gradient arena (one bucket each).  The autograd pass only stashes
+    the incoming feature gradient and the saved activations (EncoderPairFn.backward); TrainStep
+    then runs run(0), run(1), ... and all-reduces bucket k while segment k+1 computes.
+
+    Segments (reverse layer order): [ASPP + layer4], layer3 (in halves when it is deep), then
+    [layer2 + layer1 + stem]."""
+
+    def __init__(self, enc, arena):
+        self.enc = enc
+        self.arena = arena
+        self.rec = self.dfa = self.dx = None
+        bb = enc.backbone
+        l3 = list(bb.layer3)
+        l3_rev = list(reversed(l3))
+        if len(l3) > 10:
+            h = len(l3) // 2
+            mid = [l3_rev[:h], l3_rev[h:]]
+        else:
+            mid = [l3_rev]
+        # each segment: list of ("aspp" | block | "stem") in backward order
+        self.plan = ([["aspp"] + list(reversed(list(bb.layer4)))] + mid +
+                     [list(reversed(list(bb.layer2))) + list(reversed(list(bb.layer1))) + ["stem"]])
+
+    def segment_params(self, k):
+        """Parameters whose gradients segment k produces (its bucket), in production order."""
+        out = []
+        for it in self.plan[k]:
+            mod = self.enc.aspp if it == "aspp" else (self.enc.backbone if it == "stem" else it)
+            if it == "stem":
+                out += [mod.conv1.weight, mod.bn1.weight, mod.bn1.bias]
+            else:
+                out += [p for p in mod.parameters() if p.requires_grad]
+        return out
+
+    def stash(self, rec, dfa):
+        self.rec, self.dfa = rec, dfa
+
+    def run(self, k):
+        rec, grads = self.rec, GradSink(self.arena)
+        by_blk = {it[1]: it for it in rec[1:-1]}
+        for it in self.plan[k]:
+            if it == "aspp":
+                self.dx = aspp_bwd(rec[-1], self.dfa, grads)
+            elif it == "stem":
+                stem_bwd(rec[0], self.dx, grads)
+            else:
+                self.dx = bottleneck_bwd(by_blk[it], self.dx, grads)
+        if k == len(self.plan) - 1:
+            self.rec = self.dfa = self.dx = None
+        return grads
 
 
 def encode_pair(enc, img_a, img_b):

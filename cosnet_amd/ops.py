@@ -210,7 +210,7 @@ def conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg=1, bias=None
     return out, oh, ow, (mean, invstd)
 
 
-def conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn):
+def conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn, dgamma=None, dbeta=None):
     """Stride-1 conv input-gradient fused with the backward reduction of the BN + ReLU whose
     pre-activation x [n*oh*ow, cin] fed the conv (cn_conv_dgrad_bn).  Returns
     (dy_bn [P, cin], dgamma, dbeta): the gradient at the BN output and the BN's parameter
@@ -218,8 +218,10 @@ def conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn):
     cout = wt.shape[1] // (k * k)
     P = n * oh * ow
     out = torch.empty((P, cin), dtype=dy.dtype, device=dy.device)
-    dgamma = torch.empty((cin,), dtype=torch.float32, device=dy.device)
-    dbeta = torch.empty_like(dgamma)
+    if dgamma is None:
+        dgamma = torch.empty((cin,), dtype=torch.float32, device=dy.device)
+    if dbeta is None:
+        dbeta = torch.empty((cin,), dtype=torch.float32, device=dy.device)
     nws = int(nv.query("cn_conv_dgrad_bn_workspace_floats", dtc(dy), P, cin, k * k * cout))
     ws = torch.empty((nws,), dtype=torch.float32, device=dy.device)
     es = dy.element_size()
@@ -538,16 +540,20 @@ def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rb
     return out
 
 
-def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=None):
-    """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu.
+def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=None, dgamma=None,
+           dbeta=None, dprelu=None):
+    """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu
+    (dgamma / dbeta / dprelu written into the given buffers if any, e.g. gradient-arena slices).
     act=1 with y=None: the ReLU mask is recomputed from x with the forward's affine (no read of
     the activation; only valid when y = relu(bn(x)) had no residual added)."""
     p, c = x.shape
     if act == 1 and y is None:
         act = 3
-    dgamma = torch.empty((c,), dtype=torch.float32, device=x.device)
-    dbeta = torch.empty_like(dgamma)
-    dpc = torch.empty_like(dgamma) if act == 2 else None
+    if dgamma is None:
+        dgamma = torch.empty((c,), dtype=torch.float32, device=x.device)
+    if dbeta is None:
+        dbeta = torch.empty((c,), dtype=torch.float32, device=x.device)
+    dpc = torch.empty((c,), dtype=torch.float32, device=x.device) if act == 2 else None
     if want_dx and dx is None:
         dx = torch.empty((p, c), dtype=x.dtype, device=x.device)
     ws = _ws(x.dtype, p, c, x.device)
@@ -557,9 +563,9 @@ def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=N
             nv.ptr(b), act, nv.ptr(prelu), dgamma.data_ptr(), dbeta.data_ptr(), nv.ptr(dpc),
             nv.ptr(dx), ld(dx) if dx is not None else 0, nv.ptr(dres),
             ld(dres) if dres is not None else 0, ws.data_ptr(), nv.stream())
-    dprelu = None
     if dpc is not None:  # per-channel partials -> the single PReLU weight (fixed order)
-        dprelu = torch.empty((1,), dtype=torch.float32, device=x.device)
+        if dprelu is None:
+            dprelu = torch.empty((1,), dtype=torch.float32, device=x.device)
         nv.call("cn_sum_rows", dpc.data_ptr(), c, 1, dprelu.data_ptr(), nv.stream())
     return dx, dgamma, dbeta, dprelu
 

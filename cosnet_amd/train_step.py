@@ -15,23 +15,35 @@ the learning rates in a device tensor refreshed before each replay, and the BCE 
 counts (the only data-dependent scalar of the step) are computed ahead of the graph — under
 data parallelism they are all-reduced there, so the graph itself holds no collective.
 
-Data parallel (world > 1): the graph ends by packing every gradient into one flat fp32 buffer;
-the buffer is averaged with ONE RCCL all-reduce (ReduceOp.AVG, the DDP gradient semantics) and
-the SGD kernel reads its gradients straight out of it.  BN running statistics stay per rank
-during training (train-mode BN normalises with batch statistics, so they never enter the
-step); sync_buffers() broadcasts rank 0's before evaluation or checkpointing.
+Data parallel (world > 1): every gradient lives in one flat fp32 "arena" laid out in the order
+the backward produces it, cut into buckets: [head (co-attention, fusion, decoder)] then the
+depth encoder and the RGB encoder segment by segment ([ASPP + layer4], layer3 halves,
+[layer2 + layer1 + stem]).  The encoder backwards are deferred out of autograd
+(encoder_fn.DeferredEncoderBwd) and write their gradients straight into their bucket, so
+nothing is packed.  The step is recorded as a chain of HIP graphs -- forward + autograd
+backward of the head, then one graph per encoder segment, then SGD -- and each bucket's
+all-reduce (RCCL, async, pre-scaled by 1/world and summed = DataParallel's mean) is issued on
+the host as soon as its graph is queued: bucket k reduces over xGMI while segment k+1
+computes.  Optionally the buckets are reduced in bf16 (grad_dtype="bf16": half the bytes).
+BN running statistics stay per rank during training (train-mode BN normalises with batch
+statistics, so they never enter the step); sync_buffers() broadcasts rank 0's before evaluation
+or checkpointing.
 """
 import torch
 import torch.distributed as dist
 
+from . import _native as nv
 from . import functions as fn
+from . import ops
 
 
 class TrainStep:
     """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
 
-    def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None):
+    def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None,
+                 grad_dtype="fp32"):
         self.model, self.opt = model, opt
+        self.grad_dtype = grad_dtype
         self.l1 = float(l1_weight)
         self.graphed = graphed
         self.group = group
@@ -65,6 +77,7 @@ class TrainStep:
         self.flat = None
         self.graph = None
         self._nbt_delta = None
+        self.dp = None            # data-parallel state (_dp_setup)
         opt.reserve()  # pinned SGD tables + the device learning-rate tensor
 
     # ---- inputs ---------------------------------------------------------------------------
@@ -105,44 +118,122 @@ class TrainStep:
         torch.autograd.backward(loss, self._one)
         self._mem(" After backward")
         self.loss = loss.detach()
-        if self.world == 1:
-            self.opt.step()
-        else:
-            self._pack()
-
-    def _flat_views(self):
-        """fp32 flat gradient buffer + one view per parameter with the parameter's strides."""
-        n = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros((n,), dtype=torch.float32, device=self.params[0].device)
-        self.views = []
-        off = 0
-        for p in self.params:
-            v = self.flat[off:off + p.numel()].as_strided(p.shape, p.stride())
-            self.views.append(v)
-            off += p.numel()
-
-    def _pack(self):
-        grads, views = [], []
-        for p, v in zip(self.params, self.views):
-            if p.grad is not None:
-                grads.append(p.grad)
-                views.append(v)
-        torch._foreach_copy_(views, grads)
-
-    def _after_pack(self):
-        """world > 1: average the packed gradients and step SGD on them (eager, two calls)."""
-        if dist.get_backend(self.group) == "nccl":   # RCCL averages in the collective
-            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
-        else:                                           # gloo (CPU-side tests): no AVG op
-            dist.all_reduce(self.flat, group=self.group)
-            self.flat.mul_(1.0 / self.world)
-        saved = [p.grad for p in self.params]
-        for p, v in zip(self.params, self.views):
-            if p.grad is not None:
-                p.grad = v
         self.opt.step()
-        for p, g in zip(self.params, saved):
-            p.grad = g
+
+    # ---- data parallel: arena, buckets, deferred encoder backward ----------------------------
+    def _dp_setup(self):
+        from .encoder_fn import DeferredEncoderBwd
+        m = self.model
+        train = [p for p in self.params]
+        encs = [m.depth_encoder, m.encoder]          # the order their segments run in
+        defers = [DeferredEncoderBwd(e, None) for e in encs]
+        enc_ids = {id(p) for e in encs for p in e.parameters()}
+        head = [p for p in train if id(p) not in enc_ids]
+        buckets = [head]
+        segs = []
+        for d in defers:
+            for k in range(len(d.plan)):
+                ps = [p for p in d.segment_params(k) if any(p is q for q in train)]
+                buckets.append(ps)
+                segs.append((d, k))
+        got = [p for b in buckets for p in b]
+        assert len({id(p) for p in got}) == len(got), "a parameter in two buckets"
+        missing = [p for p in train if id(p) not in {id(q) for q in got}]
+        buckets[0] += missing   # trainable encoder params outside the plan (none in RAA)
+        # every slot starts on a 64-byte boundary (the per-channel kernels need 16-B alignment)
+        rnd = lambda k: (k + 15) // 16 * 16
+        n = sum(rnd(p.numel()) for b in buckets for p in b)
+        dev = train[0].device
+        flat = torch.zeros((n,), dtype=torch.float32, device=dev)
+        arena, views, ranges, off = {}, {}, [], 0
+        for b in buckets:
+            b0 = off
+            for p in b:
+                sl = flat[off:off + p.numel()]
+                arena[p] = sl
+                views[p] = sl.as_strided(p.shape, p.stride())
+                off += rnd(p.numel())
+            ranges.append((b0, off))
+        for d in defers:
+            d.arena = arena
+        for e, d in zip(encs, defers):
+            e._cn_defer = d
+        half = None
+        if self.grad_dtype == "bf16":
+            half = torch.zeros((n,), dtype=torch.bfloat16, device=dev)
+        self.dp = {"buckets": buckets, "ranges": ranges, "segs": segs, "flat": flat, "arena": arena,
+                   "views": views, "head": head, "half": half, "works": [], "graphs": None,
+                   "head_live": None}
+        self.flat = flat
+
+    def _dp_forward_backward(self):
+        """Graph A's body: forward, loss, autograd backward (encoders deferred), head bucket."""
+        dp = self.dp
+        self.opt.zero_grad()
+        x1, x2, _ = self.model(self.rgb_a, self.rgb_b, self.dep_a, self.dep_b)
+        loss = fn.BceL1PairDevFn.apply(x1, x2, self.gt_a, self.gt_b, self.cnt, self.total, self.l1)
+        self._mem(" After forward")
+        torch.autograd.backward(loss, self._one)
+        self.loss = loss.detach()
+        if dp["head_live"] is None:   # which head parameters receive a gradient (static)
+            dp["head_live"] = [p for p in dp["head"] if p.grad is not None]
+        live = dp["head_live"]
+        torch._foreach_copy_([dp["views"][p] for p in live], [p.grad for p in live])
+        self._dp_prepare_bucket(0)
+
+    def _dp_prepare_bucket(self, k):
+        """Device work that readies bucket k for its all-reduce: the 1/world pre-scale (sum of
+        scaled = DataParallel's mean) and, for bf16 reduction, the cast."""
+        dp = self.dp
+        a, b = dp["ranges"][k]
+        if b == a:
+            return
+        nv.call("cn_scale", dp["flat"][a:].data_ptr(), b - a, 1.0 / self.world, nv.stream())
+        if dp["half"] is not None:
+            ops.cast_copy(dp["flat"][a:b].view(-1, 1), dp["half"][a:b].view(-1, 1))
+
+    def _dp_segment(self, i):
+        d, k = self.dp["segs"][i]
+        d.run(k)
+        self._dp_prepare_bucket(i + 1)
+
+    def _dp_launch_reduce(self, k):
+        """Issue bucket k's all-reduce (async): RCCL waits for the work queued so far on the
+        current stream and runs beside the segments queued after it."""
+        dp = self.dp
+        a, b = dp["ranges"][k]
+        if b == a:
+            return
+        buf = dp["half"][a:b] if dp["half"] is not None else dp["flat"][a:b]
+        dp["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
+
+    def _dp_finish(self):
+        """Wait for every bucket, (cast back,) point the parameters' .grad at the arena, SGD."""
+        dp = self.dp
+        for w in dp["works"]:
+            w.wait()
+        dp["works"] = []
+        self._dp_sgd()
+
+    def _dp_sgd(self):
+        dp = self.dp
+        if dp["half"] is not None:
+            ops.cast_copy(dp["half"].view(-1, 1), dp["flat"].view(-1, 1))
+        live = set(id(p) for p in dp["head_live"])
+        for b_i, b in enumerate(dp["buckets"]):
+            for p in b:
+                if b_i > 0 or id(p) in live:
+                    p.grad = dp["views"][p]
+        self.opt.step()
+        self._mem(" After backward")
+
+    def _dp_eager_once(self):
+        self._dp_forward_backward()
+        self._dp_launch_reduce(0)
+        for i in range(len(self.dp["segs"])):
+            self._dp_segment(i)
+            self._dp_launch_reduce(i + 1)
+        self._dp_finish()
 
     # ---- capture / replay ---------------------------------------------------------------------
     def _bn_counts(self):
@@ -151,8 +242,8 @@ class TrainStep:
 
     def capture(self, warmup=2):
         """Run `warmup` eager iterations (they are real steps) on a side stream, then record."""
-        if self.world > 1:
-            self._flat_views()
+        if self.world > 1 and self.dp is None:
+            self._dp_setup()
         if not self.graphed:
             for _ in range(warmup):
                 self._eager_once()
@@ -170,11 +261,14 @@ class TrainStep:
         self.opt.refresh_lrs()
         torch.cuda.synchronize()
         before = self._bn_counts()
-        self.graph = torch.cuda.CUDAGraph()
         self._capturing = True
         try:
-            with torch.cuda.graph(self.graph, stream=s):
-                self._body()
+            if self.world > 1:
+                self._dp_capture(s)
+            else:
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph, stream=s):
+                    self._body()
         finally:
             self._capturing = False
         self._graph_loss = self.loss
@@ -184,13 +278,52 @@ class TrainStep:
             m._cn_nbt = k
         torch.cuda.synchronize()
 
+    def _dp_capture(self, s):
+        """Record the data-parallel step as a chain of graphs sharing one memory pool: A (forward
+        + autograd backward + head bucket), one per encoder segment, and SGD.  The tensors the
+        later graphs read (saved activations, the stashed feature gradients) stay referenced
+        by the deferred-backward holders, so no capture reuses their memory."""
+        dp = self.dp
+        pool = torch.cuda.graph_pool_handle()
+        keep = []
+        ga = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, stream=s, pool=pool):
+            self._dp_forward_backward()
+        segs = []
+        for i in range(len(dp["segs"])):
+            d, k = dp["segs"][i]
+            keep.append((d.rec, d.dfa))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s, pool=pool):
+                d.run(k)
+                self._dp_prepare_bucket(i + 1)
+            segs.append(g)
+        gs = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gs, stream=s, pool=pool):
+            self._dp_sgd()
+        dp["graphs"] = (ga, segs, gs, keep)
+        self.graph = ga
+
+    def _dp_replay(self):
+        dp = self.dp
+        ga, segs, gs, _ = dp["graphs"]
+        ga.replay()
+        self._dp_launch_reduce(0)
+        for i, g in enumerate(segs):
+            g.replay()
+            self._dp_launch_reduce(i + 1)
+        for w in dp["works"]:
+            w.wait()
+        dp["works"] = []
+        gs.replay()
+
     def run_batch(self, rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b, lrs):
         """One EAGER iteration on inputs of any size (the reference's augmented batches change
         H, W every batch, so they cannot replay one recorded graph)."""
         if self.graphed and self.graph is not None:
             raise RuntimeError("run_batch is the eager path; build the TrainStep with graphed=False")
-        if self.world > 1 and self.flat is None:
-            self._flat_views()
+        if self.world > 1 and self.dp is None:
+            self._dp_setup()
         b, _, h, w = rgb_a.shape
         self.rgb_a, self.rgb_b, self.dep_a, self.dep_b, self.gt_a, self.gt_b = (
             rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b)
@@ -207,12 +340,16 @@ class TrainStep:
         return self.loss
 
     def _eager_once(self):
+        if self.world > 1 and self.dp is None:
+            self._dp_setup()
+
         def once():
             self._counts()
             self.opt.refresh_lrs()
-            self._body()
             if self.world > 1:
-                self._after_pack()
+                self._dp_eager_once()
+            else:
+                self._body()
         self._on_stream(once)
 
     def __call__(self, lrs):
@@ -223,7 +360,10 @@ class TrainStep:
             return self.loss
         self.opt.refresh_lrs()
         self._counts()
-        self.graph.replay()
+        if self.world > 1:
+            self._dp_replay()
+        else:
+            self.graph.replay()
         self.loss = self._graph_loss
         self._mem(" After forward")
         self._mem(" After backward")
@@ -231,8 +371,6 @@ class TrainStep:
         # the weight cache stays valid
         for m, d in self._nbt_delta.items():
             m._cn_nbt = getattr(m, "_cn_nbt", 0) + d
-        if self.world > 1:
-            self._after_pack()
         return self.loss
 
     def sync_buffers(self, src=0):

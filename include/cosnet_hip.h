@@ -226,6 +226,8 @@ int cn_mean_rows(const float* x, int nrows, int C, float* out, hipStream_t strea
 /* Fixed-order column sums of [nrows][C] fp32 (e.g. the per-channel PReLU gradient partials of
  * deeplab/deeplabv3_encoder.py:82 -> the single PReLU weight's gradient). */
 int cn_sum_rows(const float* x, int nrows, int C, float* out, hipStream_t stream);
+/* x[i] *= s in place (the 1/world pre-scaling of a gradient bucket before its sum all-reduce) */
+int cn_scale(float* x, long long n, float s, hipStream_t stream);
 /* out[i] = x[i] * s[0], s a device scalar: chain rule of a loss gradient (autograd of
  * train.py:595-599) without a host read. */
 int cn_scale_dev(const float* x, long long n, const float* s, float* out, hipStream_t stream);

@@ -64,6 +64,8 @@ def get_arguments(argv=None):
     p.add_argument("--graph", type=int, default=1)
     p.add_argument("--duplicate-params", action="store_true")
     p.add_argument("--snapshot-root", default=".")
+    p.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="data-parallel gradient reduction dtype (bucketed, overlapped)")
     p.add_argument("--log-mem", type=int, default=1,
                    help="logMem lines around each iteration like train.py:560-621 (0: off)")
     return p.parse_args(argv)
@@ -274,7 +276,8 @@ def main(argv=None):
         db = _SbmBatches(db, args.batch_size, rank, world, args.random_seed)
     train_len = len(db)
     max_iter = args.maxEpoches * train_len
-    step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph) and not sbm)
+    step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph) and not sbm,
+                     grad_dtype=args.grad_dtype)
     mem = (lambda prefix: log_mem(logger, prefix)) if (args.log_mem and is0) else (lambda prefix: None)
     step.mem_hook = mem
     say("=====> Begin to train: %d iterations per epoch, %d epochs, %d GPU(s) x %d pairs" % (
