@@ -299,7 +299,7 @@ __device__ __forceinline__ void raw_barrier() {
 // blocks per CU, the
 // occupancy the plain kernel has from its LDS footprint; HIP's 2nd bound is waves per SIMD).
 template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0>
-__global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128) ? 4 : 1) void gemm_kernel(GemmArgs p) {
+__global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128 && S == 2) ? 4 : 1) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
   constexpr int VEC = VecOf<T>::N;
   constexpr int BK = 8 * VEC;
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
                                          // otherwise cost every plain GEMM occupancy)
   const int c0t = (tid % GPR) * 8;       // this thread's columns within the tile (fixed)
   float sk[8], sa1[8], sa2[8], sb1[8], sb2[8];
-  float bk1[8], bsf[8], bmu[8], bis[8];
+  float bk1[8], bsf[8], bmu[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sk[e] = 0.f; sa1[e] = sa2[e] = sb1[e] = sb2[e] = 0.f; }
   int segA_end = 0x7fffffff;
@@ -532,9 +532,9 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
       const bool in = c < p.N;
       const float g = in ? (p.br_gamma ? p.br_gamma[c] : 1.f) : 0.f;
       const float b = in ? (p.br_beta ? p.br_beta[c] : 0.f) : 0.f;
+      const float is = in ? p.br_invstd[c] : 0.f;
       bmu[e] = in ? p.br_mean[c] : 0.f;
-      bis[e] = in ? p.br_invstd[c] : 0.f;
-      bk1[e] = g * bis[e];              // the forward apply's affine (bn.hip bn_apply_k): the
+      bk1[e] = g * is;                  // the forward apply's affine (bn.hip bn_apply_k): the
       bsf[e] = b - bmu[e] * bk1[e];     // recomputed ReLU mask has exactly the forward's sign
     }
   }
@@ -655,10 +655,10 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
+          // sum dz * (x - mu); the invstd factor of xh is applied once per column at the end
           float dd = (col + e < p.N && fmaf(xv[e], bk1[e], bsf[e]) > 0.f) ? v[e] : 0.f;
-          const float xh = (xv[e] - bmu[e]) * bis[e];
           sa1[e] += dd;
-          sa2[e] = fmaf(dd, xh, sa2[e]);
+          sa2[e] = fmaf(dd, xv[e] - bmu[e], sa2[e]);
         }
       }
 #endif
@@ -703,6 +703,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
       float a = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) a += red[(w * 4 + q) * BN + c];
+      if (smode == 2 && q == 1 && n0 + c < p.N) a *= p.br_invstd[n0 + c];
       if (n0 + c < p.N) ws[(long long)(smode == 1 ? q + 1 : q) * p.st_plane + n0 + c] = a;
     }
     if (smode == 1 && tid < GPR) {
@@ -746,14 +747,20 @@ static long long cfg_blocks(int c, const GemmArgs& a, int batch) {
          batch * a.nsplit;
 }
 
-// Shape heuristic (tools/fwd_sweep.sh / wgrad_sweep.sh on the step's conv shapes, with the
-// K-invariant loaders): 256x256 for wide, deep products (N >= 512 and K >= 2048: the ASPP
-// atrous convs, layer-4, their dgrads) even below one block per CU; 128x64 for N <= 64;
+// Shape heuristic (tools/fwd_sweep.sh / wgrad_sweep.sh / gemm_cold.py on the step's conv
+// shapes, operands cold in HBM as in the step): 128x64 for N <= 64; 256x256 for wide, deep
+// products (N >= 512 and K >= 2048: the ASPP atrous convs, layer-4) when that still gives ~200+
+// blocks (the frame-batch layer-4 dgrad at 114 blocks runs 76 vs 120 us on 128x128); where
+// 128x128 leaves at most one block per CU (frame-batch layer-3 dgrads: 226 blocks) the 3-deep
+// ring hides the HBM latency a second resident block would (29 vs 38 us, 16 vs 21 us);
 // 128x128 with 8 waves (32x64 per wave) everywhere else.
+static long long tiles_of(int c, int M, int N) {
+  return (long long)((M + kCfg[c].bm - 1) / kCfg[c].bm) * ((N + kCfg[c].bn - 1) / kCfg[c].bn);
+}
 static int heuristic_cfg(int M, int N, int K, int bz) {
-  (void)M; (void)bz;
   if (N <= 64) return 12;
-  if (N >= 512 && K >= 2048) return 10;
+  if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 10;
+  if (tiles_of(11, M, N) * bz <= 256 && K >= 512) return 13;
   return 11;
 }
 
@@ -785,6 +792,7 @@ static int launch_epi(const GemmArgs& a, hipStream_t st) {
       case 10: return launch_c<T, T, 10, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 11: return launch_c<T, T, 11, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 12: return launch_c<T, T, 12, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 13: return launch_c<T, T, 13, LA, L_KC_DENSE, EPI>(a, 1, st);
       default: return CN_ERR_UNSUPPORTED;
     }
   }
@@ -837,7 +845,9 @@ static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_
 template <class CT, int LA>
 static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
   // (the 256x256 tile would spill its fp8 fragments: 128x128 serves the wide products too)
-  if (pick_cfg(a, batch) == 12) return launch_c<f8e4m3, CT, 12, LA, L_KC_DENSE>(a, batch, st);
+  const int c = pick_cfg(a, batch);
+  if (c == 12) return launch_c<f8e4m3, CT, 12, LA, L_KC_DENSE>(a, batch, st);
+  if (c == 13) return launch_c<f8e4m3, CT, 13, LA, L_KC_DENSE>(a, batch, st);
   return launch_c<f8e4m3, CT, 11, LA, L_KC_DENSE>(a, batch, st);
 }
 

@@ -63,6 +63,15 @@ def main():
             c = torch.empty(m_, n_, device=dev, dtype=dt)
             tg = gtime(lambda: ops.gemm(a, b, m_, n_, k_, lda=cin, ldb=cin, out=c, ldc=n_))
             res += " | dense %6.0f TF" % (2.0 * m_ * n_ * k_ / tg / 1e12)
+            # the same products through torch (hipBLASLt): fwd x.W^T, wgrad dY^T.x, dgrad dY.W
+            w2 = wf.view(cout, cin)
+            t1 = gtime(lambda: torch.mm(a, w2.t(), out=c))
+            dw2 = torch.empty(cout, cin, device=dev, dtype=dt)
+            t2 = gtime(lambda: torch.mm(yb.t(), xb, out=dw2))
+            dx2 = torch.empty_like(xb)
+            t3 = gtime(lambda: torch.mm(yb, w2, out=dx2))
+            res += " || hipBLASLt fwd %6.0f wgrad %6.0f dgrad %6.0f TF" % (
+                fl / t1 / 1e12, fl / 2 / t2 / 1e12, fl / 2 / t3 / 1e12)
         print(res, flush=True)
     print("weighted ms/step (both encoders, pair fwd, frame-a bwd):", {k: round(v * 1e3, 2) for k, v in tot.items()})
     for sz in (4096, 8192):
