@@ -57,6 +57,7 @@ class RGBDSegmentation_RAA(nn.Module):
         self.compute_dtype = torch.bfloat16
         self.fp8 = None            # Fp8Context: e4m3 forward conv GEMMs in the encoders (configs[4])
         self.pair_encoder = True   # batch frames a and b through each encoder (encoder_fn.py)
+        self.concurrent_encoders = True   # depth encoder on a second stream (forward())
         self._to_channels_last()
         self.register_state_dict_pre_hook(_flush_bn_counters)
 
@@ -139,17 +140,30 @@ class RGBDSegmentation_RAA(nn.Module):
 
     def set_fp8(self, on=True):
         """fp8 (OCP e4m3) operands for the encoders' forward conv GEMMs (cosnet_amd/fp8.py);
-        needs the bf16 compute dtype."""
+        needs the bf16 compute dtype.  The depth encoder gets a context of its own: it runs
+        concurrently with the RGB encoder, and a context's scale update covers all its states."""
         if on and self.compute_dtype != torch.bfloat16:
             raise ValueError("fp8 convs run inside the bf16 path")
         from .fp8 import Fp8Context
         self.fp8 = Fp8Context() if on else None
+        self._fp8_depth = Fp8Context() if on else None
         return self
 
     def _set_dtype(self):
         for m in self.modules():
             m._cn_dtype = self.compute_dtype
             m._cn_fp8 = self.fp8
+        for m in self.depth_encoder.modules():
+            m._cn_fp8 = getattr(self, "_fp8_depth", None)
+
+    def _side_stream(self, dev):
+        """Stream of the depth encoder (None: run it after the RGB encoder on one stream)."""
+        if not self.concurrent_encoders or dev.type != "cuda":
+            return None
+        s = getattr(self, "_cn_side", None)
+        if s is None or s.device != dev:
+            s = self._cn_side = torch.cuda.Stream(device=dev)
+        return s
 
     def forward(self, rgbs_a, rgbs_b, depths_a, depths_b, stages=None):
         self._set_dtype()
@@ -157,9 +171,26 @@ class RGBDSegmentation_RAA(nn.Module):
         input_size = tuple(rgbs_a.shape[2:])
         ng = torch.no_grad if self.no_grad_for_counterpart else _Null
         if self.no_grad_for_counterpart and self.pair_encoder and rgbs_a.shape == rgbs_b.shape:
-            # both frames in one batched encoder pass (cosnet_amd/encoder_fn.py)
-            va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
-            da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
+            # both frames in one batched encoder pass (cosnet_amd/encoder_fn.py); the depth
+            # encoder, independent of the RGB one up to the head, runs on a second stream so its
+            # kernels fill the CUs the RGB kernels leave idle (captured as a parallel graph
+            # branch; its backward follows it there -- autograd runs a backward op on its
+            # forward's stream)
+            side = self._side_stream(rgbs_a.device)
+            if side is None:
+                va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
+                da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
+            else:
+                cur = torch.cuda.current_stream(rgbs_a.device)
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
+                va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
+                cur.wait_stream(side)
+                depths_a.record_stream(side)
+                depths_b.record_stream(side)
+                da.record_stream(cur)
+                db.record_stream(cur)
         else:
             va, geo = self.encoder.features_nhwc(rgbs_a)
             with ng():
