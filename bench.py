@@ -276,12 +276,21 @@ def main():
     if prof and args.graph:
         # ROCm graphs cannot carry timing events: time the GEMM launches of one more step,
         # run eagerly right after the timed replays (same kernels, shapes and weights)
+        # (encoders on one stream here: events around a launch that overlaps the other
+        # stream's kernels would charge it their time)
+        conc = getattr(model, "concurrent_encoders", False)
+        model.concurrent_encoders = False
         with prof:
             step.eager(lrs(args.warmup + args.steps))
         torch.cuda.synchronize()
+        model.concurrent_encoders = conc
     if prof:
         n, fl, kt = prof.summary()
         nbytes = prof.algorithmic_bytes()
+        # the flash co-attention launches are reported on their own (roofline_coattention_train)
+        fn_, ffl, ft, fb = [a + b for a, b in zip(prof.select("coatt_flash_fwd"),
+                                                 prof.select("coatt_flash_bwd"))]
+        n, fl, kt, nbytes = n - fn_, fl - ffl, kt - ft, nbytes - fb
         if args.graph:  # one eager step: scale to the timed steps
             n, fl, kt, nbytes = n * args.steps, fl * args.steps, kt * args.steps, nbytes * args.steps
         peak = MFMA_BF16_PEAK_TFLOPS if dtype == torch.bfloat16 else MFMA_F32_PEAK_TFLOPS
@@ -306,6 +315,16 @@ def main():
                 "frac": ab / at / 1e9 / HBM_PEAK_GBS, "tflops": afl / at / 1e12,
                 "mfma_frac": afl / at / 1e12 / peak, "launches_per_step": an / (1 if args.graph else args.steps),
                 "bytes_per_launch": ab / an, "us_per_launch": at / an * 1e6}
+        if fn_:
+            # training co-attention (both modalities): flash forward + the two backward kernels,
+            # algorithmic FLOPs (ops.coatt_flash_fwd / coatt_flash_bwd tags)
+            sc = 1 if args.graph else args.steps
+            out["roofline_coattention_train"] = {
+                "bound": "mfma", "kernel": "coatt_flash fwd (S never in HBM, LSE kept) + dVa_t + PV backward",
+                "achieved": ffl / ft / 1e12, "peak": peak, "unit": "TFLOP/s", "frac": ffl / ft / 1e12 / peak,
+                "launches_per_step": fn_ / sc, "us_per_step": ft / sc * 1e6,
+                "fwd_tflops": prof.select("coatt_flash_fwd")[1] / max(prof.select("coatt_flash_fwd")[2], 1e-12) / 1e12,
+                "bwd_tflops": prof.select("coatt_flash_bwd")[1] / max(prof.select("coatt_flash_bwd")[2], 1e-12) / 1e12}
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if prof and dtype == torch.bfloat16 and S == 473:
         out["roofline_coattention"] = coattention_roofline(dev)

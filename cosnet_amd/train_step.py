@@ -125,17 +125,20 @@ class TrainStep:
         from .encoder_fn import DeferredEncoderBwd
         m = self.model
         train = [p for p in self.params]
-        encs = [m.depth_encoder, m.encoder]          # the order their segments run in
+        encs = [m.encoder, m.depth_encoder]
         defers = [DeferredEncoderBwd(e, None) for e in encs]
         enc_ids = {id(p) for e in encs for p in e.parameters()}
         head = [p for p in train if id(p) not in enc_ids]
         buckets = [head]
+        # stage j = RGB segment j (on the step's stream) beside depth segment j (on the model's
+        # second stream, as in the forward); one bucket per stage, all-reduced while the next
+        # stage computes
         segs = []
-        for d in defers:
-            for k in range(len(d.plan)):
-                ps = [p for p in d.segment_params(k) if any(p is q for q in train)]
-                buckets.append(ps)
-                segs.append((d, k))
+        for j in range(max(len(d.plan) for d in defers)):
+            st = [(d, j) for d in defers if j < len(d.plan)]
+            ps = [p for d, k in st for p in d.segment_params(k) if any(p is q for q in train)]
+            buckets.append(ps)
+            segs.append(st)
         got = [p for b in buckets for p in b]
         assert len({id(p) for p in got}) == len(got), "a parameter in two buckets"
         missing = [p for p in train if id(p) not in {id(q) for q in got}]
@@ -192,9 +195,24 @@ class TrainStep:
         if dp["half"] is not None:
             ops.cast_copy(dp["flat"][a:b].view(-1, 1), dp["half"][a:b].view(-1, 1))
 
+    def _dp_stage(self, i):
+        """Encoder-backward stage i: the RGB segment here, the depth segment on the side stream."""
+        st = self.dp["segs"][i]
+        side = self.model._side_stream(self.flat.device) if len(st) > 1 else None
+        if side is None:
+            for d, k in st:
+                d.run(k)
+            return
+        cur = torch.cuda.current_stream()
+        side.wait_stream(cur)
+        st[0][0].run(st[0][1])
+        with torch.cuda.stream(side):
+            for d, k in st[1:]:
+                d.run(k)
+        cur.wait_stream(side)
+
     def _dp_segment(self, i):
-        d, k = self.dp["segs"][i]
-        d.run(k)
+        self._dp_stage(i)
         self._dp_prepare_bucket(i + 1)
 
     def _dp_launch_reduce(self, k):
@@ -291,12 +309,10 @@ class TrainStep:
             self._dp_forward_backward()
         segs = []
         for i in range(len(dp["segs"])):
-            d, k = dp["segs"][i]
-            keep.append((d.rec, d.dfa))
+            keep.append([(d.rec, d.dfa) for d, _ in dp["segs"][i]])
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s, pool=pool):
-                d.run(k)
-                self._dp_prepare_bucket(i + 1)
+                self._dp_segment(i)
             segs.append(g)
         gs = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gs, stream=s, pool=pool):
