@@ -171,26 +171,35 @@ class RGBDSegmentation_RAA(nn.Module):
         input_size = tuple(rgbs_a.shape[2:])
         ng = torch.no_grad if self.no_grad_for_counterpart else _Null
         if self.no_grad_for_counterpart and self.pair_encoder and rgbs_a.shape == rgbs_b.shape:
-            # both frames in one batched encoder pass (cosnet_amd/encoder_fn.py); the depth
-            # encoder, independent of the RGB one up to the head, runs on a second stream so its
-            # kernels fill the CUs the RGB kernels leave idle (captured as a parallel graph
-            # branch; its backward follows it there -- autograd runs a backward op on its
-            # forward's stream)
+            # both frames in one batched encoder pass (cosnet_amd/encoder_fn.py).  The depth
+            # encoder and the depth branch of the head (:197-247) are independent of the RGB
+            # side up to the fusion (:251), so they run on a second stream whose kernels fill
+            # the CUs the RGB kernels leave idle (a parallel branch of the recorded graph; the
+            # backward follows -- autograd runs a backward op on its forward's stream)
             side = self._side_stream(rgbs_a.device)
-            if side is None:
-                va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
-                da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
-            else:
+            if side is not None:
                 cur = torch.cuda.current_stream(rgbs_a.device)
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
                     da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
+                    dz_a, dz_b = self._depth_head(da, db, dgeo)
                 va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
+                with torch.no_grad():
+                    labels = self.encoder.annotate_nhwc(vb, geo, input_size)   # frame b (:146)
+                z_a, z_b = self._rgb_head(va, vb, geo)
                 cur.wait_stream(side)
-                depths_a.record_stream(side)
-                depths_b.record_stream(side)
-                da.record_stream(cur)
-                db.record_stream(cur)
+                for t in (depths_a, depths_b):
+                    t.record_stream(side)
+                for t in (da, db, dz_a, dz_b):
+                    t.record_stream(cur)
+                if dgeo != geo:
+                    raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+                x1, x2 = self._decode(z_a, z_b, dz_a, dz_b, geo, input_size)
+                if stages is not None:
+                    stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
+                return x1, x2, labels
+            va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
+            da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
         else:
             va, geo = self.encoder.features_nhwc(rgbs_a)
             with ng():
@@ -212,9 +221,14 @@ class RGBDSegmentation_RAA(nn.Module):
         (rgbd_segmentation_RAA.py:150-266).  The reference interleaves the depth encoder calls
         with the RGB head (:198-203); the encoders have no data dependence on the head, so the
         order of launches does not change any result."""
+        z_a, z_b = self._rgb_head(va, vb, geo)
+        dz_a, dz_b = self._depth_head(da, db, geo)
+        return self._decode(z_a, z_b, dz_a, dz_b, geo, input_size)
+
+    def _rgb_head(self, va, vb, geo):
+        """RGB co-attention + gate + reduce conv + BN (rgbd_segmentation_RAA.py:150-191)."""
         n, h, w = geo
         hw = h * w
-        # RGB co-attention
         link = {}   # V_a's two gradient contributions meet inside CoattFn's backward
         za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw), link)
         cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False, link)
@@ -223,7 +237,12 @@ class RGBDSegmentation_RAA(nn.Module):
                             self.bn_A.weight, self.bn_A.bias, self.bn_A)
         z_b = fn.BNFn.apply(fn.ConvFn.apply(cat_b, self.reduce_channels_B.weight, None, geo, 3, 1, 1, 1),
                             self.bn_B.weight, self.bn_B.bias, self.bn_B)
-        # depth co-attention
+        return z_a, z_b
+
+    def _depth_head(self, da, db, geo):
+        """Depth co-attention + gate + reduce conv + BN + 1x1 (rgbd_segmentation_RAA.py:204-247)."""
+        n, h, w = geo
+        hw = h * w
         dlink = {}
         dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw), dlink)
         dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False, dlink)
@@ -235,7 +254,10 @@ class RGBDSegmentation_RAA(nn.Module):
             dz_b = fn.BNFn.apply(fn.ConvFn.apply(dcat_b, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
                                  self.depth_bn.weight, self.depth_bn.bias, self.depth_bn)
             dz_b = fn.ConvFn.apply(dz_b, self.depth_weights.weight, self.depth_weights.bias, geo, 1, 1, 0, 1)
-        # fusion + decoder (:251-266)
+        return dz_a, dz_b
+
+    def _decode(self, z_a, z_b, dz_a, dz_b, geo, input_size):
+        """Fusion + decoder (rgbd_segmentation_RAA.py:251-266)."""
         la = fn.HeadFn.apply(z_a, dz_a, self.segmentation_classifier_A.weight,
                              self.segmentation_classifier_A.bias, True)
         lb = fn.HeadFn.apply(z_b, dz_b, self.segmentation_classifier_B.weight,

@@ -88,3 +88,23 @@ def test_eager_after_graph_keeps_graph_tables(cuda):
     n, fl, t = prof.summary()
     assert n > 100 and fl > 0 and 0 < t < 1.0
     assert abs(l1 - l2) <= 1e-5 * abs(l1)
+
+
+@pytest.mark.gpu
+def test_two_stream_encoders_match_one_stream(cuda):
+    """The depth encoder on its own stream (forward and, through autograd, backward; a parallel
+    branch of the recorded graph) gives the step BIT-identical results to running both
+    encoders on one stream: the kernels are deterministic, only their overlap changes."""
+    runs = [_setup(cuda, torch.bfloat16, graphed=True) for _ in range(2)]
+    runs[1][0].concurrent_encoders = False
+    for _, st in runs:
+        st.opt.set_lrs(_lrs(0))
+        st.capture(warmup=1)
+    losses = [[float(st(_lrs(1 + i))) for i in range(2)] for _, st in runs]
+    torch.cuda.synchronize()
+    assert losses[0] == losses[1], losses
+    for k, (x0, x1) in enumerate(zip(_bufs(runs[0][1]), _bufs(runs[1][1]))):
+        assert torch.equal(x0, x1), (k, tuple(x0.shape))
+    p0 = [p.detach() for p in runs[0][0].parameters()]
+    p1 = [p.detach() for p in runs[1][0].parameters()]
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
