@@ -278,11 +278,17 @@ def main():
         # run eagerly right after the timed replays (same kernels, shapes and weights)
         # (encoders on one stream here: events around a launch that overlaps the other
         # stream's kernels would charge it their time)
+        # The depth parameters' AccumulateGrad nodes were created on the second stream; moving
+        # the depth encoder to the main stream for this one step is a deliberate stream change,
+        # so autograd's mismatch warning is silenced for it (and restored after).
         conc = getattr(model, "concurrent_encoders", False)
         model.concurrent_encoders = False
+        warn = torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch
+        warn(False)
         with prof:
             step.eager(lrs(args.warmup + args.steps))
         torch.cuda.synchronize()
+        warn(True)
         model.concurrent_encoders = conc
     if prof:
         n, fl, kt = prof.summary()
