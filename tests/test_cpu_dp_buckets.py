@@ -1,0 +1,88 @@
+"""The data-parallel gradient layout and bucket reduction of TrainStep (train_step.py) on CPU,
+world_size 2 over gloo: the arena/bucket plan covers every trainable parameter exactly once,
+stage j's bucket holds exactly RGB segment j + depth segment j (the order the staged encoder
+backward produces them), slots are 64-byte aligned, and the per-bucket async all-reduce sums
+the ranks' 1/world-scaled buckets into DataParallel's mean.  (The pre-scale and the SGD are
+HIP kernels; their GPU coverage is tests/test_gpu_dataparallel.py.)"""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cosnet_amd as C
+        from cosnet_amd.optim import reference_param_groups
+        from cosnet_amd.train_step import TrainStep
+
+        torch.manual_seed(0)
+        m = C.build_model(torch.float32)
+        m.encoder.main_classifier.requires_grad_(False)
+        g0, g1 = reference_param_groups(m)
+        ts = TrainStep.__new__(TrainStep)        # the planning half only (no device tables)
+        ts.model, ts.group, ts.world, ts.grad_dtype = m, None, world, "fp32"
+        seen, ts.params = set(), []
+        for p in list(g0) + list(g1):
+            if id(p) not in seen:
+                seen.add(id(p))
+                ts.params.append(p)
+        ts._dp_setup()
+        dp = ts.dp
+        got = [p for b in dp["buckets"] for p in b]
+        ok_cover = (len({id(p) for p in got}) == len(got) ==
+                    len({id(p) for p in ts.params}))
+        ok_align = all(a % 16 == 0 for a, _ in dp["ranges"])
+        ok_contig = all(dp["ranges"][i][1] == dp["ranges"][i + 1][0] for i in range(len(dp["ranges"]) - 1))
+        ok_alias = all(dp["views"][p].data_ptr() == dp["arena"][p].data_ptr() for p in got)
+        ok_stage = True
+        for j, st in enumerate(dp["segs"]):
+            encs = [type(d.enc).__name__ for d, _ in st]
+            want = [p for d, k in st for p in d.segment_params(k)
+                    if any(p is q for q in ts.params)]
+            ok_stage &= [id(p) for p in dp["buckets"][j + 1]] == [id(p) for p in want]
+            ok_stage &= encs[0] == "Encoder" and (len(st) == 1 or "Depth" in encs[1])
+        # every rank writes (rank + 1) / world into its buckets (the in-graph 1/world pre-scale),
+        # the per-bucket async all-reduce must leave the mean (1 + 2) / 2 everywhere
+        dp["flat"].fill_((rank + 1) / world)
+        for k in range(len(dp["buckets"])):
+            ts._dp_launch_reduce(k)
+        for w in dp["works"]:
+            w.wait()
+        a, b = dp["ranges"][0][0], dp["ranges"][-1][1]
+        red = dp["flat"][a:b]
+        q.put((rank, ok_cover, ok_align, ok_contig, ok_alias, ok_stage, len(dp["segs"]),
+               float(red.min()), float(red.max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucket_plan_and_reduction_two_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, cover, align, contig, alias, stage, nseg, lo, hi in res:
+        assert cover and align and contig and alias and stage, (rank, cover, align, contig, alias, stage)
+        assert nseg == 4          # RGB: ASPP+layer4, layer3 x2, layer2+1+stem; depth: 3 of them
+        assert lo == hi == 1.5, (lo, hi)

@@ -18,7 +18,7 @@ dev = torch.device('cuda:0')
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 
 
-def run(conc):
+def run(conc, prio=0):
     torch.manual_seed(0)
     m = C.build_model(torch.bfloat16)
     m.load_state_dict(recipe_state_dict(m.state_dict()))
@@ -28,6 +28,8 @@ def run(conc):
     g0, g1 = reference_param_groups(m)
     opt = SGD([g0, g1], [1e-6, 1e-5])
     st = TrainStep(m, opt, 4, 473, graphed=True)
+    if prio:
+        st.stream = torch.cuda.Stream(device=dev, priority=prio)   # RGB / critical path
     st.load(*[t.to(dev) for t in synthetic_inputs(4, 473, 473, seed=1)])
     st.capture(warmup=2)
     for _ in range(3):
@@ -43,6 +45,8 @@ def run(conc):
     return dt
 
 
-for name, conc in (("one stream", False), ("two streams", True)) * 2:
-    dt = run(conc)
+print("stream priority range", torch.cuda.Stream.priority_range())
+for name, conc, prio in (("one stream", False, 0), ("two streams", True, 0),
+                         ("two, main high", True, -1)) * 2:
+    dt = run(conc, prio)
     print("%-16s %6.2f ms/step  %6.1f pairs/s" % (name, dt * 1e3, 4 / dt), flush=True)
