@@ -285,6 +285,10 @@ def main():
         model.concurrent_encoders = False
         warn = torch.autograd.graph.set_warn_on_accumulate_grad_stream_mismatch
         warn(False)
+        # hold the device with a spin kernel while the host queues the whole eager step, so the
+        # events bracket back-to-back kernels (host launch gaps would otherwise be timed too)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(0.4 * 2.0e9))
         with prof:
             step.eager(lrs(args.warmup + args.steps))
         torch.cuda.synchronize()

@@ -32,6 +32,8 @@ def main():
     st.capture(warmup=2)
     torch.cuda.synchronize()
     prof = ops.GemmProfile()
+    m.concurrent_encoders = False        # serialized kernels: events time one launch each
+    torch.cuda._sleep(int(0.4 * 2.0e9))  # device busy while the host queues the step
     with prof:
         st.eager([1e-6, 1e-5])
     torch.cuda.synchronize()
