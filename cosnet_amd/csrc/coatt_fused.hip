@@ -71,6 +71,15 @@ struct FusedDir {
 struct FusedArgs {
   FusedDir dir[2];
   int HW, HWp, ndir, nrb, nwork, accumulate;
+  // tail key split (MODE 0, no-grad forward).  Items = (row block, batch x direction); the
+  // first nfull items run whole, one workgroup each (full rounds of the chip); each of the
+  // remaining items is split over nsplit workgroups, split s covering key tiles
+  // [s tps, (s+1) tps), which write their un-normalised O (fp32) and row (max, sum) to the
+  // partials that coatt_merge_k folds in split order -- the last, partial round of workgroups
+  // becomes a short round of short workgroups.
+  int nitems, nfull, nsplit, tps;
+  float* opart;    // [nsplit][nitems - nfull][128][256]
+  float* mlpart;   // [nsplit][nitems - nfull][128][2]
 };
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
@@ -105,10 +114,20 @@ void coatt_fused_fwd_k(FusedArgs a) {
   // XCD-aware work order: hardware places workgroup i on XCD i % 8, so give each XCD a
   // contiguous run of the (batch, direction)-major work list -- the row blocks of one
   // (batch, direction) then share its K/V stream (3.7 MB) in that XCD's 4 MB L2.
-  const int per_xcd = (a.nwork + 7) >> 3;
-  const int work = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  if (work >= a.nwork) return;
-  const int rb = work % a.nrb, bd = work / a.nrb;
+  const int nfull8 = (a.nfull + 7) & ~7;
+  int item, split = 0;
+  if ((int)blockIdx.x < nfull8) {
+    const int per_xcd = nfull8 >> 3;
+    item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (item >= a.nfull) return;
+  } else {
+    const int t = blockIdx.x - nfull8;
+    item = a.nfull + t / a.nsplit;
+    split = t % a.nsplit;
+    if (item >= a.nitems) return;
+  }
+  const bool part = item >= a.nfull;   // a split of a tail item
+  const int rb = item % a.nrb, bd = item / a.nrb;
   const FusedDir d = a.dir[bd % a.ndir];
   const int HW = a.HW;
   const long long b = bd / a.ndir;
@@ -133,10 +152,12 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
   // K/V tile DMA: chunk p = 256 i + tid of the 1024-chunk image -> key row p >> 5, position
   // p & 31; the source chunk is the position XOR the image's swizzle.
+  const int ntiles = (HW + FBK - 1) / FBK;
+  const int tb = part ? split * a.tps : 0;   // first key tile of this work item
   auto issue = [&](int t, int stage) {
     char* kb = lds + FQB + stage * 2 * FTILE;
     char* vb = kb + FTILE;
-    const int key0 = t * FBK;
+    const int key0 = (tb + t) * FBK;
 #pragma unroll
     for (int i = 0; i < FTILE / 4096; ++i) {
       const int p = i * 256 + tid;
@@ -151,7 +172,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
     }
   };
 
-  const int nt = (HW + FBK - 1) / FBK;
+  const int nt = part ? min(ntiles - tb, a.tps) : ntiles;
   issue(0, 0);
   if (nt > 1) issue(1, 1);
 
@@ -189,7 +210,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
     // of the S MFMAs so their latency hides under them
     f32x4 nk[4];
     if constexpr (MODE == 1) {
-      const float* kl = d.klse + b * a.HWp + t * FBK + 4 * h;
+      const float* kl = d.klse + b * a.HWp + (tb + t) * FBK + 4 * h;
 #pragma unroll
       for (int q = 0; q < 4; ++q) nk[q] = *(const f32x4*)(kl + 8 * q);
     }
@@ -254,7 +275,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
     }
 
     // ---- online softmax over the keys (register i: key 32t + (i&3) + 8(i>>2) + 4h)
-    const int key0 = t * FBK;
+    const int key0 = (tb + t) * FBK;
     bf16x8 pf[2];
     if constexpr (MODE == 1) {
 #pragma unroll
@@ -345,6 +366,20 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
   // ---- epilogue: O[qrow][d] = o / l ; register i of d tile dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
   l += __shfl_xor(l, 32, 64);
+  if (MODE == 0 && part) {
+    // key split: un-normalised partial O and (m, l) of this split, folded by coatt_merge_k
+    if (qrow < HW) {
+      const long long prow = ((long long)split * (a.nitems - a.nfull) + (item - a.nfull)) * FBQ + (qrow - q0);
+      float* op = a.opart + prow * FD + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          *(f32x4*)(op + 32 * dt + 8 * c) = f32x4{o[dt][4 * c], o[dt][4 * c + 1], o[dt][4 * c + 2], o[dt][4 * c + 3]};
+      if (h == 0) *(float2*)(a.mlpart + prow * 2) = float2{m, l};
+    }
+    return;
+  }
   if (MODE == 0 && d.lse && h == 0 && qrow < a.HWp)
     d.lse[b * a.HWp + qrow] = qrow < HW ? m + __builtin_amdgcn_logf(l) : INFINITY;  // logf = log2
   if (qrow < HW) {
@@ -369,19 +404,92 @@ void coatt_fused_fwd_k(FusedArgs a) {
   }
 }
 
+// Fold the key-split partials of one row of a tail item: O = sum_s 2^(m_s - M) O_s /
+// sum_s 2^(m_s - M) l_s, splits in order (deterministic).  One thread = 8 channels of one row.
+__global__ __launch_bounds__(256) void coatt_merge_k(FusedArgs a) {
+  const long long t = blockIdx.x * 256ll + threadIdx.x;
+  const long long rows = (long long)(a.nitems - a.nfull) * FBQ;   // rows per split slab
+  if (t >= rows * (FD / 8)) return;
+  const long long row = t / (FD / 8);
+  const int c0 = (int)(t % (FD / 8)) * 8;
+  const int item = a.nfull + (int)(row / FBQ);
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const int q = rb * FBQ + (int)(row % FBQ);
+  if (q >= a.HW) return;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const long long b = bd / a.ndir;
+  const long long sstride = rows;
+  float M = -INFINITY;
+  for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.mlpart[(s * sstride + row) * 2]);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float L = 0.f;
+  for (int s = 0; s < a.nsplit; ++s) {
+    const float2 ml = *(const float2*)(a.mlpart + (s * sstride + row) * 2);
+    const float wgt = ml.y > 0.f ? __builtin_amdgcn_exp2f(ml.x - M) : 0.f;
+    L = fmaf(ml.y, wgt, L);
+    const float* op = a.opart + (s * sstride + row) * FD + c0;
+    const f32x4 v0 = *(const f32x4*)op, v1 = *(const f32x4*)(op + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[e] = fmaf(v0[e], wgt, acc[e]);
+      acc[4 + e] = fmaf(v1[e], wgt, acc[4 + e]);
+    }
+  }
+  const float inv = 1.f / L;
+  bf16x8 outv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) outv[e] = (bf16)(acc[e] * inv);
+  *(bf16x8*)(d.o + (b * a.HW + q) * d.ldo + c0) = outv;
+  if (d.lse && c0 == 0) d.lse[b * a.HWp + q] = M + __builtin_amdgcn_logf(L);
+}
+
 }  // namespace
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Tail split for `items` workgroup-sized work items at one workgroup per CU: the items of the
+// last, partial round of 256 (all of them when there are fewer) are split over up to
+// 256 / tail workgroups each (>= 16 key tiles per split).
+static void plan_split(int items, int ntiles, int* nfull, int* nsplit) {
+  *nfull = items;
+  *nsplit = 1;
+  const int rem = items % 256;   // the partial round (all of it when items < 256)
+  if (rem == 0) return;
+  int s = 256 / rem;
+  if (s > 8) s = 8;
+  while (s > 1 && ntiles / s < 16) --s;
+  if (s < 2) return;
+  *nfull = items - rem;
+  *nsplit = s;
+}
+
 static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   a.ndir = nd;
   a.nrb = (a.HW + FBQ - 1) / FBQ;
-  a.nwork = a.nrb * B * nd;
-  dim3 grid(((a.nwork + 7) / 8) * 8);
+  a.nitems = a.nrb * B * nd;
+  if (a.nsplit < 2) { a.nsplit = 1; a.nfull = a.nitems; }
+  const int ntiles = (a.HW + FBK - 1) / FBK;
+  a.tps = (ntiles + a.nsplit - 1) / a.nsplit;
+  const int nfull8 = (a.nfull + 7) & ~7;
+  a.nwork = nfull8 + (a.nitems - a.nfull) * a.nsplit;
+  dim3 grid(a.nwork);
   if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
   CN_CHECK_LAUNCH();
+  if (mode == 0 && a.nsplit > 1) {
+    const long long threads = (long long)(a.nitems - a.nfull) * FBQ * (FD / 8);
+    hipLaunchKernelGGL(coatt_merge_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a);
+    CN_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+extern "C" size_t cn_coatt_fused_workspace_bytes(int B, int HW, int ndir) {
+  const int nrb = (HW + FBQ - 1) / FBQ;
+  int nfull, s;
+  plan_split(nrb * B * ndir, (HW + FBK - 1) / FBK, &nfull, &s);
+  if (s == 1) return 0;
+  return (size_t)s * (nrb * B * ndir - nfull) * FBQ * (FD + 2) * sizeof(float);
 }
 
 static int fused_check(const void* q, long long ldq, const void* k, long long ldk, const void* v,
@@ -398,6 +506,33 @@ extern "C" int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void*
                                   void* zb, long long ld_z, hipStream_t st) {
   return cn_coatt_flash_fwd(vat, ld_vat, va, ld_va, vb, ld_vb, B, HW, C, za, zb, ld_z, nullptr,
                             nullptr, st);
+}
+
+extern "C" int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                     const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                                     void* zb, long long ld_z, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (B <= 0 || HW <= 0) return CN_ERR_SHAPE;
+  int rc = fused_check(vat, ld_vat, vb, ld_vb, va, ld_va, ld_z, C);
+  if (rc) return rc;
+  if (((uintptr_t)za & 7) || ((uintptr_t)zb & 7)) return CN_ERR_ALIGN;
+  FusedArgs a = {};
+  int nd = 0;
+  if (za) a.dir[nd++] = FusedDir{(const bf16*)vat, (const bf16*)vb, (const bf16*)vb, (bf16*)za, ld_vat, ld_vb, ld_vb, ld_z, nullptr, nullptr};
+  if (zb) a.dir[nd++] = FusedDir{(const bf16*)vb, (const bf16*)vat, (const bf16*)va, (bf16*)zb, ld_vb, ld_vat, ld_va, ld_z, nullptr, nullptr};
+  if (nd == 0) return CN_ERR_SHAPE;
+  a.HW = HW;
+  a.HWp = (HW + 31) / 32 * 32;
+  const int nrb = (HW + FBQ - 1) / FBQ;
+  plan_split(nrb * B * nd, (HW + FBK - 1) / FBK, &a.nfull, &a.nsplit);
+  // the merge writes 16-byte rows: unsplit when the outputs are not laid out for that
+  if (((uintptr_t)za & 15) || ((uintptr_t)zb & 15) || (ld_z % 8)) a.nsplit = 1;
+  if (a.nsplit > 1) {
+    const size_t tail_rows = (size_t)a.nsplit * (nrb * B * nd - a.nfull) * FBQ;
+    if (!ws || ws_bytes < tail_rows * (FD + 2) * sizeof(float) || !aligned16(ws)) return CN_ERR_SHAPE;
+    a.opart = (float*)ws;
+    a.mlpart = a.opart + tail_rows * FD;
+  }
+  return fused_launch(0, a, B, nd, st);
 }
 
 extern "C" int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,

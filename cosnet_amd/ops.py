@@ -408,8 +408,12 @@ def coatt_fused(vat, va, vb, n, hw, za=None, zb=None):
     c = vat.shape[1]
     ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_fused", n, hw, c),
                      (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
-    nv.call("cn_coatt_fused_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
-            ld(vb), n, hw, c, nv.ptr(za), nv.ptr(zb), ld(za if za is not None else zb), nv.stream())
+    ndir = (za is not None) + (zb is not None)
+    nws = int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, ndir))
+    ws = torch.empty((nws // 4,), dtype=torch.float32, device=vat.device) if nws else None
+    nv.call("cn_coatt_fused_fwd_ws", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
+            ld(vb), n, hw, c, nv.ptr(za), nv.ptr(zb), ld(za if za is not None else zb), nv.ptr(ws),
+            nws, nv.stream())
     _prof_end(ev)
     return za, zb
 

@@ -169,6 +169,16 @@ int cn_coatt_dscore(int dtype, const void* Pc, const float* dPc, const float* d1
 int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
                        const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                        long long ld_z, hipStream_t stream);
+/* Same product with the keys split over several workgroups per query block when one
+ * workgroup per (row block, pair, direction) would leave most of the last round of CUs idle
+ * (configs[3]: 5 pairs -> 290 workgroups on 256 CUs): each split writes its un-normalised
+ * fp32 partial O and row (max, sum) into ws, a merge kernel folds them in split order.
+ * ws_bytes >= cn_coatt_fused_workspace_bytes(B, HW, ndir) (0: no split, ws may be NULL);
+ * za/zb 16-byte aligned, ld_z % 8 == 0. */
+size_t cn_coatt_fused_workspace_bytes(int B, int HW, int ndir);
+int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                          const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                          long long ld_z, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* Flash-style co-attention for TRAINING (rgbd_segmentation_RAA.py:160-170 and its autograd),
  * S never in HBM.  Forward = cn_coatt_fused_fwd plus the per-row log2-sum-exp2 of each direction
