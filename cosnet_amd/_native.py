@@ -60,6 +60,10 @@ _SIGS = {
     "cn_coatt_flash_pv": (_I, [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _P, _L, _I, _P]),
     "cn_coatt_flash_dvat": (_I, [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _I, _I, _I, _P,
                                  _L, _I, _P]),
+    "cn_coatt_flash_dvat_ws": (_I, [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _I, _I, _I, _P,
+                                    _L, _I, _P, _S, _P]),
+    "cn_coatt_flash_bwd_workspace_bytes": (_S, [_I, _I]),
+    "cn_coatt_flash_pv_ws": (_I, [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _P, _L, _I, _P, _S, _P]),
     "cn_rowdot_seg": (_I, [_I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _P]),
     "cn_nchw_to_nhwc": (_I, [_I, _P, _I, _I, _I, _I, _I, _P, _P]),
     "cn_weight_prep": (_I, [_I, _P, _I, _I, _I, _I, _P, _P, _P]),

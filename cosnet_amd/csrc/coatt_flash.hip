@@ -71,6 +71,10 @@ struct BwdArgs {
   const float* lse_b; const float* d1;                // per key        [B][HWp] (+inf padded), [B][HWp]
   bf16* out; long long ld_out;                        // dVa_t rows i
   int HW, HWp, nrb, nwork, accumulate;
+  // key split (fewer row blocks than CUs): split s sums keys of tiles [s tps, (s+1) tps) into
+  // fp32 partials part[s][B*HW][256]; dvat_sum_k adds them in split order
+  int nsplit, tps;
+  float* part;
 };
 
 // T0: the P0 (softmax over j) term, T1: the P1 (softmax over i) term.
@@ -87,8 +91,9 @@ void coatt_flash_dvat_k(BwdArgs a) {
   const int per_xcd = (a.nwork + 7) >> 3;
   const int work = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
   if (work >= a.nwork) return;
-  const int rb = work % a.nrb;
-  const long long b = work / a.nrb;
+  const int rb = work % a.nrb, rest = work / a.nrb;
+  const int split = rest % a.nsplit;
+  const long long b = rest / a.nsplit;
   const int HW = a.HW;
   const int q0 = rb * BQ;
   const int qrow = q0 + w * 32 + r;
@@ -128,9 +133,11 @@ void coatt_flash_dvat_k(BwdArgs a) {
   const bf16* KV = a.vb + b * HW * a.ld_vb;
   const bf16* K2 = T1 ? a.dzb + b * HW * a.ld_dzb : nullptr;
   // per tile: [Vb rows | Vb transposed | dZb rows]
+  const int ntiles = (HW + BK - 1) / BK;
+  const int tb = split * a.tps;   // first key tile of this work item
   auto issue = [&](int t, int stage) {
     char* kb = lds + QB + stage * STG;
-    const int key0 = t * BK;
+    const int key0 = (tb + t) * BK;
 #pragma unroll
     for (int i = 0; i < TILE / 4096; ++i) {
       const int p = i * 256 + tid;
@@ -149,7 +156,7 @@ void coatt_flash_dvat_k(BwdArgs a) {
     }
   };
 
-  const int nt = (HW + BK - 1) / BK;
+  const int nt = min(ntiles - tb, a.tps);
   issue(0, 0);
   if (NST > 2 && nt > 1) issue(1, 1);
 
@@ -171,16 +178,17 @@ void coatt_flash_dvat_k(BwdArgs a) {
     // the next DMA so their wait does not drain it
     f32x4 nk[4], nd[4];
     if constexpr (T1) {
-      const float* kl = a.lse_b + b * a.HWp + t * BK + 4 * h;
-      const float* kd = a.d1 + b * a.HWp + t * BK + 4 * h;
+      const int kt = tb + t;
+      const float* kl = a.lse_b + b * a.HWp + kt * BK + 4 * h;
+      const float* kd = a.d1 + b * a.HWp + kt * BK + 4 * h;
 #pragma unroll
       for (int q = 0; q < 4; ++q) { nk[q] = *(const f32x4*)(kl + 8 * q); nd[q] = *(const f32x4*)(kd + 8 * q); }
-      if ((t + 1) * BK > HW) {  // D1's padding is not written: zero it (lse_b's is +inf)
+      if ((kt + 1) * BK > HW) {  // D1's padding is not written: zero it (lse_b's is +inf)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (t * BK + 8 * q + 4 * h + j >= HW) nd[q][j] = 0.f;
+            if (kt * BK + 8 * q + 4 * h + j >= HW) nd[q][j] = 0.f;
       }
     }
     // the stage of tile t + NST - 1 was last read in iteration t-1, which every wave has passed
@@ -268,7 +276,14 @@ void coatt_flash_dvat_k(BwdArgs a) {
   }
 
   // ---- epilogue: dVa_t[qrow][d]; register i of d tile dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
-  if (qok) {
+  if (qok && a.nsplit > 1) {   // fp32 partial of this key split
+    float* op = a.part + (((long long)split * (a.nwork / (a.nrb * a.nsplit)) + b) * HW + qrow) * BD + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *(f32x4*)(op + 32 * dt + 8 * c) = f32x4{o[dt][4 * c], o[dt][4 * c + 1], o[dt][4 * c + 2], o[dt][4 * c + 3]};
+  } else if (qok) {
     bf16* op = a.out + (b * HW + qrow) * a.ld_out + 4 * h;
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
@@ -289,9 +304,57 @@ void coatt_flash_dvat_k(BwdArgs a) {
   }
 }
 
+// out[row][c..c+7] (+)= sum_s part[s][row][c..c+7], splits in order.  One thread = 8 channels.
+__global__ __launch_bounds__(256) void dvat_sum_k(const float* __restrict__ part, int nsplit, long long rows,
+                                                  bf16* out, long long ld_out, int accumulate) {
+  const long long t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= rows * (BD / 8)) return;
+  const long long row = t / (BD / 8);
+  const int c0 = (int)(t % (BD / 8)) * 8;
+  float acc[8];
+  bf16* op = out + row * ld_out + c0;
+  if (accumulate) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = (float)op[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  }
+  for (int s = 0; s < nsplit; ++s) {
+    const float* p = part + ((long long)s * rows + row) * BD + c0;
+    const f32x4 v0 = *(const f32x4*)p, v1 = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { acc[e] += v0[e]; acc[4 + e] += v1[e]; }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) op[e] = (bf16)acc[e];
+}
+
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Key splits for `items` workgroups when they leave CUs idle (one workgroup per CU): up to
+// 256 / items splits of >= 16 key tiles each.
+int bwd_nsplit(int items, int ntiles) {
+  if (items >= 256) return 1;
+  int s = 256 / items;
+  if (s > 8) s = 8;
+  while (s > 1 && ntiles / s < 16) --s;
+  return s;
+}
+
 }  // namespace
+
+extern "C" size_t cn_coatt_flash_bwd_workspace_bytes(int B, int HW) {
+  const int s = bwd_nsplit(((HW + BQ - 1) / BQ) * B, (HW + BK - 1) / BK);
+  return s > 1 ? (size_t)s * B * HW * BD * sizeof(float) : 0;
+}
+
+extern "C" int cn_coatt_flash_dvat_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                      const void* dza, long long ld_dza, const void* vb, long long ld_vb,
+                                      const void* dzb, long long ld_dzb, const float* lse_a,
+                                      const float* d0, const float* lse_b, const float* d1, int B,
+                                      int HW, int C, void* out, long long ld_out, int accumulate,
+                                      void* ws, size_t ws_bytes, hipStream_t st);
 
 extern "C" int cn_coatt_flash_dvat(const void* vat, long long ld_vat, const void* va, long long ld_va,
                                    const void* dza, long long ld_dza, const void* vb, long long ld_vb,
@@ -299,6 +362,16 @@ extern "C" int cn_coatt_flash_dvat(const void* vat, long long ld_vat, const void
                                    const float* d0, const float* lse_b, const float* d1, int B,
                                    int HW, int C, void* out, long long ld_out, int accumulate,
                                    hipStream_t st) {
+  return cn_coatt_flash_dvat_ws(vat, ld_vat, va, ld_va, dza, ld_dza, vb, ld_vb, dzb, ld_dzb, lse_a,
+                                d0, lse_b, d1, B, HW, C, out, ld_out, accumulate, nullptr, 0, st);
+}
+
+extern "C" int cn_coatt_flash_dvat_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                      const void* dza, long long ld_dza, const void* vb, long long ld_vb,
+                                      const void* dzb, long long ld_dzb, const float* lse_a,
+                                      const float* d0, const float* lse_b, const float* d1, int B,
+                                      int HW, int C, void* out, long long ld_out, int accumulate,
+                                      void* ws, size_t ws_bytes, hipStream_t st) {
   if (C != BD || B <= 0 || HW <= 0 || !out) return CN_ERR_SHAPE;
   const bool t0 = dza != nullptr, t1 = dzb != nullptr;
   if (!t0 && !t1) return CN_ERR_SHAPE;
@@ -317,12 +390,26 @@ extern "C" int cn_coatt_flash_dvat(const void* vat, long long ld_vat, const void
   a.out = (bf16*)out; a.ld_out = ld_out;
   a.HW = HW; a.HWp = (HW + 31) / 32 * 32;
   a.nrb = (HW + BQ - 1) / BQ;
-  a.nwork = a.nrb * B;
+  const int ntiles = (HW + BK - 1) / BK;
+  a.nsplit = bwd_nsplit(a.nrb * B, ntiles);
+  // the split sum writes 16-byte rows; without a workspace run unsplit
+  const size_t need = (size_t)a.nsplit * B * HW * BD * sizeof(float);
+  if (a.nsplit > 1 && (!ws || ws_bytes < need || !al16(ws) || ((uintptr_t)out & 15) || ld_out % 8))
+    a.nsplit = 1;
+  a.tps = (ntiles + a.nsplit - 1) / a.nsplit;
+  a.part = (float*)ws;
+  a.nwork = a.nrb * B * a.nsplit;
   a.accumulate = accumulate;
   dim3 grid(((a.nwork + 7) / 8) * 8);
   if (t0 && t1) hipLaunchKernelGGL((coatt_flash_dvat_k<true, true>), grid, dim3(256), 0, st, a);
   else if (t0) hipLaunchKernelGGL((coatt_flash_dvat_k<true, false>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((coatt_flash_dvat_k<false, true>), grid, dim3(256), 0, st, a);
   CN_CHECK_LAUNCH();
+  if (a.nsplit > 1) {
+    const long long rows = (long long)B * HW;
+    hipLaunchKernelGGL(dvat_sum_k, dim3((unsigned)((rows * (BD / 8) + 255) / 256)), dim3(256), 0, st,
+                       (const float*)ws, a.nsplit, rows, (bf16*)out, ld_out, accumulate);
+    CN_CHECK_LAUNCH();
+  }
   return 0;
 }

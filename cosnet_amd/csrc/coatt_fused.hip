@@ -366,8 +366,9 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
   // ---- epilogue: O[qrow][d] = o / l ; register i of d tile dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
   l += __shfl_xor(l, 32, 64);
-  if (MODE == 0 && part) {
-    // key split: un-normalised partial O and (m, l) of this split, folded by coatt_merge_k
+  if (part) {
+    // key split: un-normalised partial O (and MODE 0: the row's (m, l)) of this split, folded by
+    // coatt_merge_k
     if (qrow < HW) {
       const long long prow = ((long long)split * (a.nitems - a.nfull) + (item - a.nfull)) * FBQ + (qrow - q0);
       float* op = a.opart + prow * FD + 4 * h;
@@ -376,7 +377,7 @@ void coatt_fused_fwd_k(FusedArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           *(f32x4*)(op + 32 * dt + 8 * c) = f32x4{o[dt][4 * c], o[dt][4 * c + 1], o[dt][4 * c + 2], o[dt][4 * c + 3]};
-      if (h == 0) *(float2*)(a.mlpart + prow * 2) = float2{m, l};
+      if (MODE == 0 && h == 0) *(float2*)(a.mlpart + prow * 2) = float2{m, l};
     }
     return;
   }
@@ -406,6 +407,8 @@ void coatt_fused_fwd_k(FusedArgs a) {
 
 // Fold the key-split partials of one row of a tail item: O = sum_s 2^(m_s - M) O_s /
 // sum_s 2^(m_s - M) l_s, splits in order (deterministic).  One thread = 8 channels of one row.
+// MODE 1 (per-key normaliser, linear in the keys): O (+)= sum_s O_s.
+template <int MODE>
 __global__ __launch_bounds__(256) void coatt_merge_k(FusedArgs a) {
   const long long t = blockIdx.x * 256ll + threadIdx.x;
   const long long rows = (long long)(a.nitems - a.nfull) * FBQ;   // rows per split slab
@@ -419,6 +422,23 @@ __global__ __launch_bounds__(256) void coatt_merge_k(FusedArgs a) {
   const FusedDir d = a.dir[bd % a.ndir];
   const long long b = bd / a.ndir;
   const long long sstride = rows;
+  if constexpr (MODE == 1) {
+    float acc[8];
+    bf16* op = d.o + (b * a.HW + q) * d.ldo + c0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = a.accumulate ? (float)op[e] : 0.f;
+    for (int s = 0; s < a.nsplit; ++s) {
+      const float* p = a.opart + (s * sstride + row) * FD + c0;
+      const f32x4 v0 = *(const f32x4*)p, v1 = *(const f32x4*)(p + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { acc[e] += v0[e]; acc[4 + e] += v1[e]; }
+    }
+    bf16x8 outv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) outv[e] = (bf16)acc[e];
+    *(bf16x8*)op = outv;
+    return;
+  }
   float M = -INFINITY;
   for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, a.mlpart[(s * sstride + row) * 2]);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -476,9 +496,11 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
   CN_CHECK_LAUNCH();
-  if (mode == 0 && a.nsplit > 1) {
+  if (a.nsplit > 1) {
     const long long threads = (long long)(a.nitems - a.nfull) * FBQ * (FD / 8);
-    hipLaunchKernelGGL(coatt_merge_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a);
+    const dim3 g((unsigned)((threads + 255) / 256));
+    if (mode == 0) hipLaunchKernelGGL(coatt_merge_k<0>, g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(coatt_merge_k<1>, g, dim3(256), 0, st, a);
     CN_CHECK_LAUNCH();
   }
   return 0;
@@ -556,9 +578,10 @@ extern "C" int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void*
   return fused_launch(0, a, B, nd, st);
 }
 
-extern "C" int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk,
-                                 const void* v, long long ldv, const float* klse, int B, int HW,
-                                 int C, void* o, long long ldo, int accumulate, hipStream_t st) {
+extern "C" int cn_coatt_flash_pv_ws(const void* q, long long ldq, const void* k, long long ldk,
+                                    const void* v, long long ldv, const float* klse, int B, int HW,
+                                    int C, void* o, long long ldo, int accumulate, void* ws,
+                                    size_t ws_bytes, hipStream_t st) {
   if (B <= 0 || HW <= 0 || !klse || !o) return CN_ERR_SHAPE;
   int rc = fused_check(q, ldq, k, ldk, v, ldv, ldo, C);
   if (rc) return rc;
@@ -568,5 +591,19 @@ extern "C" int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, lo
   a.HW = HW;
   a.HWp = (HW + 31) / 32 * 32;
   a.accumulate = accumulate;
+  const int nrb = (HW + FBQ - 1) / FBQ;
+  plan_split(nrb * B, (HW + FBK - 1) / FBK, &a.nfull, &a.nsplit);
+  if (((uintptr_t)o & 15) || (ldo % 8)) a.nsplit = 1;
+  if (a.nsplit > 1) {
+    const size_t tail_rows = (size_t)a.nsplit * (nrb * B - a.nfull) * FBQ;
+    if (!ws || ws_bytes < tail_rows * FD * sizeof(float) || !aligned16(ws)) a.nsplit = 1;
+    a.opart = (float*)ws;
+  }
   return fused_launch(1, a, B, 1, st);
+}
+
+extern "C" int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk,
+                                 const void* v, long long ldv, const float* klse, int B, int HW,
+                                 int C, void* o, long long ldo, int accumulate, hipStream_t st) {
+  return cn_coatt_flash_pv_ws(q, ldq, k, ldk, v, ldv, klse, B, HW, C, o, ldo, accumulate, nullptr, 0, st);
 }

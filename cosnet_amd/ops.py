@@ -456,17 +456,21 @@ def coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw, dva=
     nterm = (dza is not None) + (dzb is not None)
     ev = _prof_start((1 + 2 * nterm) * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
                      (2 + 2 * nterm) * P * c * vat.element_size())
-    nv.call("cn_coatt_flash_dvat", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), nv.ptr(dza),
+    # one workspace for the key-split partials of both kernels (they run one after the other)
+    nws = max(int(nv.query("cn_coatt_flash_bwd_workspace_bytes", n, hw)),
+              int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, 1)) if dva is not None else 0)
+    ws = torch.empty((nws // 4,), dtype=torch.float32, device=dev) if nws else None
+    nv.call("cn_coatt_flash_dvat_ws", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), nv.ptr(dza),
             ld(dza) if dza is not None else c, vb.data_ptr(), ld(vb), nv.ptr(dzb),
             ld(dzb) if dzb is not None else c, lse_a.data_ptr(), nv.ptr(d0), lse_b.data_ptr(),
-            nv.ptr(d1), n, hw, c, dvat.data_ptr(), ld(dvat), 0, nv.stream())
+            nv.ptr(d1), n, hw, c, dvat.data_ptr(), ld(dvat), 0, nv.ptr(ws), nws, nv.stream())
     _prof_end(ev)
     if dva is not None and dzb is not None:
         ev = _prof_start(2 * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
                          3 * P * c * vat.element_size())
-        nv.call("cn_coatt_flash_pv", vat.data_ptr(), ld(vat), vb.data_ptr(), ld(vb), dzb.data_ptr(),
+        nv.call("cn_coatt_flash_pv_ws", vat.data_ptr(), ld(vat), vb.data_ptr(), ld(vb), dzb.data_ptr(),
                 ld(dzb), lse_b.data_ptr(), n, hw, c, dva.data_ptr(), ld(dva), int(dva_accumulate),
-                nv.stream())
+                nv.ptr(ws), nws, nv.stream())
         _prof_end(ev)
     return dvat
 

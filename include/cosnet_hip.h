@@ -194,6 +194,12 @@ int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void* va, long l
 int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk, const void* v,
                       long long ldv, const float* klse, int B, int HW, int C, void* o, long long ldo,
                       int accumulate, hipStream_t stream);
+/* Same, with a workspace (>= cn_coatt_fused_workspace_bytes(B, HW, 1)) that lets the keys of
+ * an under-filled last round of workgroups be split over several workgroups (fp32 partials
+ * summed in split order); without one (NULL / too small) it runs unsplit. */
+int cn_coatt_flash_pv_ws(const void* q, long long ldq, const void* k, long long ldk, const void* v,
+                         long long ldv, const float* klse, int B, int HW, int C, void* o,
+                         long long ldo, int accumulate, void* ws, size_t ws_bytes, hipStream_t stream);
 
 /* Backward of the flash co-attention: dva_t (+)= sum_j dS[i][j] vb[j] with
  *   dS = P0 (dza[i].vb[j] - d0[i]) + P1 (va[i].dzb[j] - d1[j]),
@@ -206,6 +212,17 @@ int cn_coatt_flash_dvat(const void* vat, long long ld_vat, const void* va, long 
                         const void* dzb, long long ld_dzb, const float* lse_a, const float* d0,
                         const float* lse_b, const float* d1, int B, int HW, int C, void* out,
                         long long ld_out, int accumulate, hipStream_t stream);
+/* Same, with a workspace (>= cn_coatt_flash_bwd_workspace_bytes(B, HW)): when the B x
+ * ceil(HW/128) row blocks leave CUs idle, the keys are split over up to 8 workgroups per row
+ * block whose fp32 partial sums are added in split order (out 16-byte aligned, ld_out % 8 == 0;
+ * otherwise, or without a workspace, unsplit). */
+size_t cn_coatt_flash_bwd_workspace_bytes(int B, int HW);
+int cn_coatt_flash_dvat_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                           const void* dza, long long ld_dza, const void* vb, long long ld_vb,
+                           const void* dzb, long long ld_dzb, const float* lse_a, const float* d0,
+                           const float* lse_b, const float* d1, int B, int HW, int C, void* out,
+                           long long ld_out, int accumulate, void* ws, size_t ws_bytes,
+                           hipStream_t stream);
 
 /* ---- memory-bound helpers -------------------------------------------------------------- */
 int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp, void* y,
