@@ -26,6 +26,21 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
 PMC_FILE = os.path.join(REPO, "profiles", "r02_pmc_step_traffic.json")
+ROCPROF_FILE = os.path.join(REPO, "profiles", "r02_rocprof_kernel_stats_bench_b4_473_final.csv")
+
+
+def rocprof_avg_us(substr):
+    """Average launch duration of a kernel family in the committed rocprofv3 --stats summary of
+    this same bench command (the cross-check of the live HIP-event timing)."""
+    try:
+        import csv
+        with open(ROCPROF_FILE) as f:
+            rows = [r for r in csv.DictReader(f) if substr in r["Name"]]
+        n = sum(int(r["Calls"]) for r in rows)
+        return {"avg_launch_us": sum(float(r["TotalDurationNs"]) for r in rows) / n / 1e3,
+                "launches": n, "source": os.path.relpath(ROCPROF_FILE, REPO)} if n else None
+    except (OSError, KeyError, ValueError):
+        return None
 FLOP_PER_PAIR_473 = 4.1364e12    # SURVEY.md §8d (flop_counter on the reference graph)
 
 
@@ -312,6 +327,8 @@ def main():
                            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": pmc["source"] if pmc else None,
                            "algorithmic_bytes_per_launch": nbytes / n,
+                           "event_avg_launch_us": kt / n * 1e6,
+                           "rocprof": rocprof_avg_us("gemm_kernel"),
                            "launches_per_step": n / args.steps,
                            "gemm_time_frac_of_step": kt / dt,
                            "gemm_tflop_per_step": fl / args.steps / 1e12}
