@@ -70,5 +70,35 @@ def main():
     print("(one chain = %d launches of a 226-block GEMM)" % L)
 
 
+def two_graphs_main():
+    """The same two chains captured as two single-stream graphs, replayed on two streams."""
+    a, b = chain(), chain()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    gs = []
+    for fn, s in ((a, sa), (b, sb)):
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            fn()
+        gs.append(g)
+    torch.cuda.synchronize()
+
+    def rep():
+        cur = torch.cuda.current_stream()
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+        with torch.cuda.stream(sa):
+            gs[0].replay()
+        with torch.cuda.stream(sb):
+            gs[1].replay()
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+    print("two single-stream graphs  %.3f ms" % timed(rep), flush=True)
+
+
 if __name__ == "__main__":
     main()
+    two_graphs_main()
