@@ -294,6 +294,9 @@ __device__ __forceinline__ void raw_barrier() {
 #ifndef CN_GEMM_PRIO
 #define CN_GEMM_PRIO 0
 #endif
+#ifndef CN_GEMM_ZREMAP
+#define CN_GEMM_ZREMAP 1
+#endif
 
 // BN-epilogue variants of the 128-row tiles keep <= 128 VGPRs (4 waves per SIMD = two 512-thread
 // blocks per CU, the
@@ -320,15 +323,31 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   // XCD-aware tile order (guide §5.5 T1, bijective form): blocks are dealt round-robin over
   // the 8 XCDs, so remap the linear id to give every XCD a contiguous run of M-tiles that
   // share the same B (weight) panel in its private L2.
-  int tm, tn;
+  // The remap runs over the whole grid, z (batch / K split) included, z-major: the blocks of one
+  // K split (or batch entry) land on one XCD, which then streams that split's A and B slices
+  // through its L2 once (split-K weight gradients: 16-36 tiles per split, 1-2.3 MB per slice)
+  // instead of every XCD re-reading every split's panels.
+  int tm, tn, bz;
   {
     const int nwg = gridDim.x * gridDim.y;
+#if CN_GEMM_ZREMAP
+    const int all = nwg * gridDim.z;
+    const int orig = blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * nwg;
+#else
+    const int all = nwg;
     const int orig = blockIdx.x + blockIdx.y * gridDim.x;
-    int lin = orig;
-    if (nwg >= 16) {
-      const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-      lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+#endif
+    int glin = orig;
+    if (all >= 16) {
+      const int xcd = orig & 7, q = all >> 3, r = all & 7;
+      glin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
     }
+#if CN_GEMM_ZREMAP
+    bz = glin / nwg;
+#else
+    bz = blockIdx.z;
+#endif
+    const int lin = glin - (glin / nwg) * nwg;
 #if CN_GEMM_GROUP_M > 0
     // grouped order: each run of GROUP_M M-tiles walks all its N-tiles before the next run,
     // so the blocks resident on one XCD share A panels (and the B panel) in its L2
@@ -347,7 +366,6 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
 #endif
   }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int bz = blockIdx.z;
   const int batch = bz / p.nsplit, split = bz - batch * p.nsplit;
   const int kbeg = split * p.k_chunk;
   const int kend = min(p.K, kbeg + p.k_chunk);
