@@ -17,13 +17,18 @@ template <class T> __device__ __forceinline__ void stv(T* p, const float* f) {
 template <class T>
 __global__ void nchw_to_nhwc_k(const float* __restrict__ x, int N, int C, int H, int W, int Cp,
                                T* __restrict__ y) {
+  // one pixel per thread: coalesced channel-plane reads, the pixel's Cp (% VEC == 0) channels
+  // written as whole 16-byte chunks
+  constexpr int V = VecOf<T>::N;
   long long total = (long long)N * H * W;
   for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
        p += (long long)gridDim.x * blockDim.x) {
     long long n = p / ((long long)H * W), hw = p - n * H * W;
-    for (int c = 0; c < Cp; ++c) {
-      float v = c < C ? x[(n * C + c) * H * W + hw] : 0.f;
-      y[p * Cp + c] = fromf<T>(v);
+    for (int c0 = 0; c0 < Cp; c0 += V) {
+      float f[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) f[v] = c0 + v < C ? x[(n * C + c0 + v) * H * W + hw] : 0.f;
+      *(u32x4*)(y + p * Cp + c0) = Chunk<T>::pack(f);
     }
   }
 }
@@ -64,22 +69,54 @@ __global__ void maxpool_fwd_k(const T* __restrict__ x, int N, int H, int W, int 
     int bi[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) { best[v] = -INFINITY; bi[v] = 0; }
-    for (int r = 0; r < k; ++r) {
-      int yy = oy * s - pad + r;
-      if (yy < 0 || yy >= H) continue;
-      for (int c = 0; c < k; ++c) {
-        int xx = ox * s - pad + c;
-        if (xx < 0 || xx >= W) continue;
+    if (k == 3) {
+      // the stem's 3x3 window: all nine 16-byte loads issued before the first compare (taps
+      // outside the image are skipped exactly as below: scan order and tie-breaking unchanged)
+      u32x4 raw[9];
+      bool in[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = oy * s - pad + t / 3, xx = ox * s - pad + t % 3;
+        in[t] = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        raw[t] = in[t] ? *(const u32x4*)(x + (((long long)n * H + yy) * W + xx) * C + cc * V)
+                       : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (!in[t]) continue;
         float f[V];
-        ldv(x + (((long long)n * H + yy) * W + xx) * C + cc * V, f);
+        Chunk<T>::unpack(raw[t], f);
 #pragma unroll
         for (int v = 0; v < V; ++v)
-          if (f[v] > best[v] || (f[v] != f[v])) { best[v] = f[v]; bi[v] = r * k + c; }
+          if (f[v] > best[v] || (f[v] != f[v])) { best[v] = f[v]; bi[v] = t; }
+      }
+    } else {
+      for (int r = 0; r < k; ++r) {
+        int yy = oy * s - pad + r;
+        if (yy < 0 || yy >= H) continue;
+        for (int c = 0; c < k; ++c) {
+          int xx = ox * s - pad + c;
+          if (xx < 0 || xx >= W) continue;
+          float f[V];
+          ldv(x + (((long long)n * H + yy) * W + xx) * C + cc * V, f);
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+            if (f[v] > best[v] || (f[v] != f[v])) { best[v] = f[v]; bi[v] = r * k + c; }
+        }
       }
     }
     stv(y + p * C + cc * V, best);
+    // the V argmax bytes of this chunk in one store (V = 8: 8 B, V = 4: 4 B; C % V == 0)
+    unsigned lo = 0, hi = 0;
 #pragma unroll
-    for (int v = 0; v < V; ++v) am[p * C + cc * V + v] = (unsigned char)bi[v];
+    for (int v = 0; v < 4; ++v) lo |= (unsigned)(bi[v] & 0xff) << (8 * v);
+    if constexpr (V == 8) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) hi |= (unsigned)(bi[4 + v] & 0xff) << (8 * v);
+      *(u32x2*)(am + p * C + cc * V) = u32x2{lo, hi};
+    } else {
+      *(unsigned*)(am + p * C + cc * V) = lo;
+    }
   }
 }
 
@@ -421,13 +458,17 @@ __global__ void upsample_sigmoid_k(const float* __restrict__ in, int N, int h, i
   }
 }
 
-// d in[n,y,x] = sum over output pixels of dout * s(1-s) * wy * wx (gather; deterministic)
-__global__ void upsample_sigmoid_bwd_k(const float* __restrict__ dout, const float* __restrict__ out,
-                                       int N, int h, int w, int H, int W, float sh, float sw,
-                                       int apply_sigmoid, float* __restrict__ din) {
+// d in[n,y,x] = sum over output pixels of dout * s(1-s) * wy * wx (gather; deterministic).
+// One wave per input pixel: its lanes stride the (Y, X) window of output pixels whose source
+// interval touches it (~17 x 17 at 60 -> 473), then a fixed xor-shuffle tree adds the lanes.
+__global__ __launch_bounds__(256) void upsample_sigmoid_bwd_k(const float* __restrict__ dout,
+                                                             const float* __restrict__ out, int N,
+                                                             int h, int w, int H, int W, float sh,
+                                                             float sw, int apply_sigmoid,
+                                                             float* __restrict__ din) {
+  const int lane = threadIdx.x & 63;
   long long total = (long long)N * h * w;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  for (long long i = blockIdx.x * 4ll + (threadIdx.x >> 6); i < total; i += gridDim.x * 4ll) {
     int x = (int)(i % w);
     long long q = i / w;
     int y = (int)(q % h);
@@ -441,26 +482,25 @@ __global__ void upsample_sigmoid_bwd_k(const float* __restrict__ dout, const flo
     if (Xlo < 0) Xlo = 0;
     if (Yhi > H - 1) Yhi = H - 1;
     if (Xhi > W - 1) Xhi = W - 1;
+    const int nX = Xhi - Xlo + 1, nk = (Yhi - Ylo + 1) * nX;
     float acc = 0.f;
-    for (int Y = Ylo; Y <= Yhi; ++Y) {
-      int y0, y1;
-      float ly;
+    for (int k = lane; k < nk; k += 64) {
+      const int Y = Ylo + k / nX, X = Xlo + k % nX;
+      int y0, y1, x0, x1;
+      float ly, lx;
       src_index(Y, h, H, sh, y0, y1, ly);
-      float wy = (y0 == y ? 1.f - ly : 0.f) + (y1 == y ? ly : 0.f);
-      if (wy == 0.f) continue;
-      for (int X = Xlo; X <= Xhi; ++X) {
-        int x0, x1;
-        float lx;
-        src_index(X, w, W, sw, x0, x1, lx);
-        float wx = (x0 == x ? 1.f - lx : 0.f) + (x1 == x ? lx : 0.f);
-        if (wx == 0.f) continue;
-        long long o = ((long long)n * H + Y) * W + X;
-        float g = dout[o];
-        if (apply_sigmoid) { float s = out[o]; g *= s * (1.f - s); }
-        acc = fmaf(g, wy * wx, acc);
-      }
+      src_index(X, w, W, sw, x0, x1, lx);
+      const float wy = (y0 == y ? 1.f - ly : 0.f) + (y1 == y ? ly : 0.f);
+      const float wx = (x0 == x ? 1.f - lx : 0.f) + (x1 == x ? lx : 0.f);
+      if (wy == 0.f || wx == 0.f) continue;
+      const long long o = ((long long)n * H + Y) * W + X;
+      float g = dout[o];
+      if (apply_sigmoid) { float s = out[o]; g *= s * (1.f - s); }
+      acc = fmaf(g, wy * wx, acc);
     }
-    din[i] = acc;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) din[i] = acc;
   }
 }
 
@@ -471,13 +511,22 @@ __global__ void zero_u64_k(unsigned long long* p, long long n) {
     p[i] = 0ull;
 }
 
-__global__ void count_ge_k(const float* __restrict__ gt, long long n, float thr, unsigned long long* cnt) {
-  unsigned long long c = 0;
+// #(gt >= thr): per-thread counts, a block reduction, ONE integer atomic per block (a few
+// hundred blocks: same-address atomics serialise, so one per wave would dominate)
+__global__ __launch_bounds__(256) void count_ge_k(const float* __restrict__ gt, long long n, float thr,
+                                                 unsigned long long* cnt) {
+  unsigned c = 0;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x)
-    c += gt[i] >= thr ? 1ull : 0ull;
+    c += gt[i] >= thr ? 1u : 0u;
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+  __shared__ unsigned wsum[4];
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = (unsigned long long)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(cnt, t);
+  }
 }
 
 // partial[block] = sum of per-element loss; dpred = d loss / d pred (already / n, * gscale)
@@ -736,6 +785,7 @@ inline int nblocks(long long n, int per = 256) {
 
 extern "C" int cn_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int Cp,
                                void* y, hipStream_t st) {
+  if (Cp % (dtype == DT_BF16 ? 8 : 4) || ((uintptr_t)y & 15)) return CN_ERR_ALIGN;
   long long n = (long long)N * H * W;
   if (dtype == DT_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_k<bf16>, dim3(nblocks(n)), dim3(256), 0, st, x, N, C, H, W, Cp, (bf16*)y);
@@ -963,7 +1013,7 @@ extern "C" int cn_upsample_sigmoid_bwd(const float* dout, const float* out, int 
                                        int H, int W, int apply_sigmoid, float* din, hipStream_t st) {
   float sh = (float)h / (float)H, sw = (float)w / (float)W;
   long long n = (long long)N * h * w;
-  hipLaunchKernelGGL(upsample_sigmoid_bwd_k, dim3(nblocks(n)), dim3(256), 0, st, dout, out, N, h, w, H, W, sh, sw, apply_sigmoid, din);
+  hipLaunchKernelGGL(upsample_sigmoid_bwd_k, dim3(nblocks(n, 4)), dim3(256), 0, st, dout, out, N, h, w, H, W, sh, sw, apply_sigmoid, din);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -971,7 +1021,7 @@ extern "C" int cn_upsample_sigmoid_bwd(const float* dout, const float* out, int 
 extern "C" int cn_count_ge(const float* gt, long long n, float thr, unsigned long long* cnt, hipStream_t st) {
   hipLaunchKernelGGL(zero_u64_k, dim3(1), dim3(64), 0, st, cnt, 1ll);
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(count_ge_k, dim3(nblocks(n)), dim3(256), 0, st, gt, n, thr, cnt);
+  hipLaunchKernelGGL(count_ge_k, dim3(nblocks(n, 256 * 16) < 256 ? nblocks(n, 256 * 16) : 256), dim3(256), 0, st, gt, n, thr, cnt);
   CN_CHECK_LAUNCH();
   return 0;
 }

@@ -663,3 +663,18 @@ def test_conv_fwd_fp8(cuda, case):
     got = nchw(y, n, oh, ow).double().cpu()
     err = ((got - ref).abs().max() / ref.abs().max()).item()
     assert err <= 1e-2, err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c", [3, 1])
+def test_nchw_to_nhwc(cuda, dt, c):
+    """cn_nchw_to_nhwc: the encoders' input frames (fp32 NCHW, rgbd_segmentation_RAA.py:143-148)
+    to zero-padded 8-channel NHWC rows in the compute dtype -- exact."""
+    n, h, w = 2, 37, 53
+    x = torch.randn((n, c, h, w), generator=torch.Generator().manual_seed(11)).to(cuda)
+    y = torch.full((n * h * w, 8), 7.0, dtype=dt, device=cuda)
+    assert nv.call("cn_nchw_to_nhwc", nv.dtype_code(dt), x.data_ptr(), n, c, h, w, 8, y.data_ptr(),
+                   nv.stream()) == 0
+    ref = torch.zeros((n * h * w, 8), dtype=dt)
+    ref[:, :c] = nhwc(x.cpu()).to(dt)
+    assert torch.equal(y.cpu(), ref)
