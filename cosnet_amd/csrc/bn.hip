@@ -161,23 +161,24 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const T* __restrict__ x,
     const int step = S * L.RPB;
     for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += SUNR * step) {
       float f[SUNR][V];
+      // SUNR independent 16-B loads in flight per thread: every load is issued unconditionally
+      // (rows past P re-read row 0 and contribute zero), so no branch separates them -- a
+      // bounds branch per load made hipcc drain vmcnt(0) after each one
 #pragma unroll
-      for (int u = 0; u < SUNR; ++u) {  // SUNR independent 16-B loads in flight per thread
+      for (int u = 0; u < SUNR; ++u) {
         const int r = r0 + u * step;
-        if (r < P) ld_chunk(xs + (long long)r * ld + chunk * V, f[u]);
-        else {
-#pragma unroll
-          for (int v = 0; v < V; ++v) f[u][v] = K[v];
-        }
+        ld_chunk(xs + (long long)(r < P ? r : 0) * ld + chunk * V, f[u]);
       }
 #pragma unroll
-      for (int u = 0; u < SUNR; ++u)
+      for (int u = 0; u < SUNR; ++u) {
+        const bool in = r0 + u * step < P;
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-          float d = f[u][v] - K[v];
+          float d = in ? f[u][v] - K[v] : 0.f;
           s[v] += d;
           ss[v] = fmaf(d, d, ss[v]);
         }
+      }
     }
   }
   block_col_sums<V, 2>(L, tx, ty, s, ss, nullptr, ws + (long long)seg * 2 * S * C, S, C);
@@ -380,10 +381,11 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
   const int step = gridDim.y * L.RPB;
   for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
     float f[UNR][V], q[UNR][V];
+    // all loads of the UNR rows issued unconditionally (rows past P re-read the segment's first
+    // row and are not stored): no bounds branch between them
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const long long r = row0 + r0 + u * step;
-      if (r0 + u * step >= P) break;
+      const long long r = row0 + (r0 + u * step < P ? r0 + u * step : 0);
       ld_chunk(x + r * ldx + c0, f[u]);
       if (res) ld_chunk(res + r * ldr + c0, q[u]);
       if (xr) ld_chunk(xr + r * ldxr + c0, q[u]);
@@ -450,20 +452,30 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
     const int step = gridDim.y * L.RPB;
     for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
       float xf[UNR][V], d[UNR][V], yf[UNR][V];
+      // loads issued unconditionally (rows past P re-read row 0 and contribute zero); the
+      // activation branch sits outside the unrolled loop so no branch separates the loads
+      if (act == 1) {
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int r = r0 + u * step;
-        if (r >= P) break;
-        ld_chunk(x + (long long)r * ldx + c0, xf[u]);
-        ld_chunk(dy + (long long)r * lddy + c0, d[u]);
-        if (act == 1) ld_chunk(y + (long long)r * ldy + c0, yf[u]);
+        for (int u = 0; u < UNR; ++u) {
+          const int r = r0 + u * step < P ? r0 + u * step : 0;
+          ld_chunk(x + (long long)r * ldx + c0, xf[u]);
+          ld_chunk(dy + (long long)r * lddy + c0, d[u]);
+          ld_chunk(y + (long long)r * ldy + c0, yf[u]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int r = r0 + u * step < P ? r0 + u * step : 0;
+          ld_chunk(x + (long long)r * ldx + c0, xf[u]);
+          ld_chunk(dy + (long long)r * lddy + c0, d[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        if (r0 + u * step >= P) break;
+        const bool in = r0 + u * step < P;
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-          float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
+          float dd = (!in || (act == 1 && !(yf[u][v] > 0.f))) ? 0.f : d[u][v];
           if (act == 3 && !(fmaf(xf[u][v], sc[v], sf[v]) > 0.f)) dd = 0.f;
           float xh = (xf[u][v] - mu[v]) * is[v];
           if (NQ > 2) {
@@ -530,13 +542,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   const int step = gridDim.y * L.RPB;
   for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
     float xf[UNR][V], d[UNR][V], yf[UNR][V];
+    // loads issued unconditionally (rows past P re-read row 0 and are not stored); the
+    // activation branch sits outside the unrolled loop so no branch separates the loads
+    if (act == 1) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int r = r0 + u * step;
-      if (r >= P) break;
-      ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
-      ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
-      if (act == 1) ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * step < P ? r0 + u * step : 0;
+        ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
+        ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
+        ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * step < P ? r0 + u * step : 0;
+        ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
+        ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
