@@ -179,11 +179,19 @@ __global__ __launch_bounds__(256) void avgpool_partial_k(const T* __restrict__ x
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
   if (cc * V < C) {
-    for (int r = r0 + rg; r < r1; r += 4) {
-      float f[V];
-      ldv(x + ((long long)n * HW + r) * ld + cc * V, f);
+    // 4 rows' loads in flight per thread (rows past the range re-read row r and add +0), added
+    // in row order as before: bitwise the same sums
+    for (int r = r0 + rg; r < r1; r += 16) {
+      float f[4][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += f[v];
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r + 4 * u < r1 ? r + 4 * u : r;
+        ldv(x + ((long long)n * HW + rr) * ld + cc * V, f[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += r + 4 * u < r1 ? f[u][v] : 0.f;
     }
   }
 #pragma unroll
@@ -740,11 +748,20 @@ __global__ void colsum_k(const T* __restrict__ x, long long ld, int P, int C, fl
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
   if (cc * V < C) {
-    for (int r = blockIdx.y * 4 + rg; r < P; r += gridDim.y * 4) {
-      float f[V];
-      ldv(x + (long long)r * ld + cc * V, f);
+    // 4 rows' loads in flight per thread (rows past P re-read row r and add +0), added in row
+    // order as before: bitwise the same sums
+    const int st = gridDim.y * 4;
+    for (int r = blockIdx.y * 4 + rg; r < P; r += 4 * st) {
+      float f[4][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += f[v];
+      for (int u = 0; u < 4; ++u) {
+        const int rr = r + u * st < P ? r + u * st : r;
+        ldv(x + (long long)rr * ld + cc * V, f[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += r + u * st < P ? f[u][v] : 0.f;
     }
   }
   __shared__ float red[4][64][8];
