@@ -47,6 +47,9 @@ constexpr int FDMA = 2 * FTILE / 4096;  // LDS-DMA instructions per thread per K
 #ifndef RESCALE_T
 #define RESCALE_T 8.0f
 #endif
+#ifndef CF_DMA_SPREAD
+#define CF_DMA_SPREAD 1
+#endif
 
 __device__ __attribute__((aligned(16))) unsigned g_zero16_fused[4];
 
@@ -154,22 +157,24 @@ void coatt_fused_fwd_k(FusedArgs a) {
   // p & 31; the source chunk is the position XOR the image's swizzle.
   const int ntiles = (HW + FBK - 1) / FBK;
   const int tb = part ? split * a.tps : 0;   // first key tile of this work item
-  auto issue = [&](int t, int stage) {
+  // piece i (< FTILE / 4096) of tile t's K and V images: one 1-KB LDS-DMA per wave for each
+  auto issue_piece = [&](int t, int stage, int i) {
     char* kb = lds + FQB + stage * 2 * FTILE;
     char* vb = kb + FTILE;
     const int key0 = (tb + t) * FBK;
+    const int p = i * 256 + tid;
+    const int row = p >> 5, cpos = p & 31;
+    const int key = key0 + row;
+    const bool ok = key < HW;
+    const bf16* ks = K + (long long)key * d.ldk + ((cpos ^ (row & 15)) << 3);
+    const bf16* vs = V + (long long)key * d.ldv + ((cpos ^ ((row & 3) << 2)) << 3);
+    const int wb = (i * 256 + (tid & ~63)) * 16;
+    glds16f(ok ? (const void*)ks : zp, kb + wb);
+    glds16f(ok ? (const void*)vs : zp, vb + wb);
+  };
+  auto issue = [&](int t, int stage) {
 #pragma unroll
-    for (int i = 0; i < FTILE / 4096; ++i) {
-      const int p = i * 256 + tid;
-      const int row = p >> 5, cpos = p & 31;
-      const int key = key0 + row;
-      const bool ok = key < HW;
-      const bf16* ks = K + (long long)key * d.ldk + ((cpos ^ (row & 15)) << 3);
-      const bf16* vs = V + (long long)key * d.ldv + ((cpos ^ ((row & 3) << 2)) << 3);
-      const int wb = (i * 256 + (tid & ~63)) * 16;
-      glds16f(ok ? (const void*)ks : zp, kb + wb);
-      glds16f(ok ? (const void*)vs : zp, vb + wb);
-    }
+    for (int i = 0; i < FTILE / 4096; ++i) issue_piece(t, stage, i);
   };
 
   const int nt = part ? min(ntiles - tb, a.tps) : ntiles;
@@ -197,9 +202,13 @@ void coatt_fused_fwd_k(FusedArgs a) {
     if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(FDMA) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier_f();
-    // the stage of tile t+2 was last read in iteration t-1, which every wave has finished
-#ifndef CF_NO_DMA
-    if (t + 2 < nt) issue(t + 2, st2);
+    // the stage of tile t+2 was last read in iteration t-1, which every wave has finished.
+    // CF_DMA_SPREAD: its pieces are issued between the PV MFMAs below (a DMA piece costs its wave
+    // 60-185 issue cycles; beside the MFMAs that cost hides) instead of as a burst here.
+    const bool dodma = t + 2 < nt;
+    const int dst2 = st2;
+#if !CF_DMA_SPREAD
+    if (dodma) issue(t + 2, st2);
 #endif
     const char* kb = lds + FQB + st * 2 * FTILE;
     st = st == FSTAGES - 1 ? 0 : st + 1;
@@ -359,6 +368,9 @@ void coatt_fused_fwd_k(FusedArgs a) {
         o[it >> 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, pf[it & 1], o[it >> 1], 0, 0, 0);
 #else
         o[it >> 1][it] += (float)cur[0] * (float)pf[it & 1][1];
+#endif
+#if CF_DMA_SPREAD
+        if ((it & 1) && (it >> 1) < FTILE / 4096 && dodma) issue_piece(t + 2, dst2, it >> 1);
 #endif
       }
     }
