@@ -61,6 +61,8 @@ def parse():
                     help="data-parallel gradient buckets reduced in fp32 (default) or bf16")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the multi-rank path on one device (not a measurement)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group plumbing only (no model, no GPU)")
     return ap.parse_args()
 
 
@@ -182,12 +184,68 @@ def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):
             "executed_tflops": 4 / 3 * alg / t / 1e12, "us_per_launch": t * 1e6}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(n, argv):
+    """--gpus N outside a torch.distributed launcher: start one rank per GPU as a CHILD
+    `torch.distributed.run` (nothing in this process has touched the GPU, and it is never
+    exec-replaced); rank 0's JSON line reaches stdout through the inherited descriptor.
+    Reference: train.py:491-496 (DataParallel over --gpus), here one process per GPU."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the launcher / process-group / max-over-ranks timing plumbing of this bench
+    without the model (CPU gloo; used by tests/test_cli.py to check the N-rank launch)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher plumbing only)", "value": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "max_rank_seconds": dt,
+                          "config": {"parallelism": "dp%d" % world}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print("[bench] note: --gpus %d but WORLD_SIZE=%d; the launcher's world size is used"
+              % (args.gpus, world), file=sys.stderr)
+    rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dist_backend == "gloo":   # rehearsal: every rank on device 0

@@ -562,9 +562,13 @@ extern "C" int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const vo
   if (((uintptr_t)za & 15) || ((uintptr_t)zb & 15) || (ld_z % 8)) a.nsplit = 1;
   if (a.nsplit > 1) {
     const size_t tail_rows = (size_t)a.nsplit * (nrb * B * nd - a.nfull) * FBQ;
-    if (!ws || ws_bytes < tail_rows * (FD + 2) * sizeof(float) || !aligned16(ws)) return CN_ERR_SHAPE;
-    a.opart = (float*)ws;
-    a.mlpart = a.opart + tail_rows * FD;
+    // no (or a too small / misaligned) workspace: the unsplit launch, as the _ws siblings do
+    if (!ws || ws_bytes < tail_rows * (FD + 2) * sizeof(float) || !aligned16(ws)) {
+      a.nsplit = 1;
+    } else {
+      a.opart = (float*)ws;
+      a.mlpart = a.opart + tail_rows * FD;
+    }
   }
   return fused_launch(0, a, B, nd, st);
 }

@@ -35,9 +35,12 @@ class Fp8Weights:
     """fp8 copies of fp32 conv weights (channels_last), refreshed after each optimiser step."""
 
     def __init__(self):
-        self._c = {}          # id(w) -> [wf8, state, tag, weakref]
+        self._c = {}          # id(w) -> [wf8, state, tag, w]
         self._table = None
         self._table_n = 0
+        self._table_ptrs = None   # the master / copy addresses the table was packed with
+        self._captured = False    # a recorded graph replays the current table
+        self._graph_tables = []   # tables read by recorded graphs: kept for their lifetime
 
     @staticmethod
     def _tag(w):
@@ -46,6 +49,9 @@ class Fp8Weights:
     def get(self, w):
         e = self._c.get(id(w))
         if e is None:
+            if self._captured:
+                raise RuntimeError("new fp8 weight after a graph captured this context's "
+                                   "refresh table (re-capture the step)")
             cout = w.shape[0]
             k = w.numel() // cout
             wf8 = torch.empty((cout, k), dtype=torch.uint8, device=w.device)
@@ -61,12 +67,24 @@ class Fp8Weights:
             e[2] = self._tag(w)
         return e[0], e[1]
 
+    def _ptrs(self):
+        return tuple((e[3].data_ptr(), e[0].data_ptr(), e[1].data_ptr()) for e in self._c.values())
+
     def refresh_all(self):
         """Re-quantise every fp8 copy from its (just updated) master: 3 launches."""
         if not self._c:
             return
+        capturing = torch.cuda.is_current_stream_capturing()
+        ptrs = self._ptrs()
+        if self._table is not None and ptrs != self._table_ptrs:
+            # a master's storage was replaced (p.data = ..., re-materialisation): the packed
+            # table would refresh from the old buffer
+            if self._captured or capturing:
+                raise RuntimeError("fp8 weight storage moved after its refresh table was "
+                                   "recorded in a graph (re-capture the step)")
+            self._table = None
         if self._table is None:
-            if torch.cuda.is_current_stream_capturing():
+            if capturing:
                 raise RuntimeError("fp8 weight table must be built before graph capture")
             blob = b""
             for wf8, st, _, w in self._c.values():
@@ -77,6 +95,10 @@ class Fp8Weights:
             dev = next(iter(self._c.values()))[0].device
             self._table = host.to(dev)
             self._table_n = len(self._c)
+            self._table_ptrs = ptrs
+        if capturing:
+            self._captured = True
+            self._graph_tables.append(self._table)
         nv.call("cn_fp8_quant_multi", self._table.data_ptr(), self._table_n, nv.stream())
         for e in self._c.values():
             e[2] = self._tag(e[3]) if e[3] is not None else None
@@ -160,7 +182,14 @@ class Fp8Context:
 LIVE = weakref.WeakSet()
 
 
-def refresh_all_weights():
-    """After an optimiser step: re-quantise every live context's fp8 weight copies."""
-    for ctx in list(LIVE):
+def contexts_of(params):
+    """The live fp8 contexts holding a weight copy of any of `params` (an optimiser's own)."""
+    ids = {id(p) for p in params}
+    return [ctx for ctx in list(LIVE) if any(k in ids for k in ctx.weights._c)]
+
+
+def refresh_weights_of(params):
+    """After an optimiser step: re-quantise the fp8 copies of the contexts whose weights this
+    optimiser trains -- never another model's (its table is not tied to this step's graph)."""
+    for ctx in contexts_of(params):
         ctx.weights.refresh_all()

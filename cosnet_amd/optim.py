@@ -205,8 +205,8 @@ class SGD:
         for ent in refreshed:
             WCACHE.refreshed(ent)
         # fp8 copies (configs[4]): re-quantised from the new masters, 3 launches for all
-        from .fp8 import refresh_all_weights
-        refresh_all_weights()
+        from .fp8 import refresh_weights_of
+        refresh_weights_of(p for g in self.groups for p in g)
 
     def _upload_lrs(self, dev):
         if self._lr_dev is None:

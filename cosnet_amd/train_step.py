@@ -198,16 +198,22 @@ class TrainStep:
     def _dp_stage(self, i):
         """Encoder-backward stage i: the RGB segment here, the depth segment on the side stream."""
         st = self.dp["segs"][i]
-        side = self.model._side_stream(self.flat.device) if len(st) > 1 else None
+        # the stream follows the ENCODER, not the position in the stage: the depth segments'
+        # saved activations were allocated on the side stream by the forward
+        depth = getattr(self.model.depth_encoder, "_cn_defer", None)
+        on_side = [(d, k) for d, k in st if d is depth]
+        here = [(d, k) for d, k in st if d is not depth]
+        side = self.model._side_stream(self.flat.device) if on_side else None
         if side is None:
             for d, k in st:
                 d.run(k)
             return
         cur = torch.cuda.current_stream()
         side.wait_stream(cur)
-        st[0][0].run(st[0][1])
+        for d, k in here:
+            d.run(k)
         with torch.cuda.stream(side):
-            for d, k in st[1:]:
+            for d, k in on_side:
                 d.run(k)
         cur.wait_stream(side)
 

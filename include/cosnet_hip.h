@@ -174,7 +174,8 @@ int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long l
  * (configs[3]: 5 pairs -> 290 workgroups on 256 CUs): each split writes its un-normalised
  * fp32 partial O and row (max, sum) into ws, a merge kernel folds them in split order.
  * ws_bytes >= cn_coatt_fused_workspace_bytes(B, HW, ndir) (0: no split, ws may be NULL);
- * za/zb 16-byte aligned, ld_z % 8 == 0. */
+ * za/zb 16-byte aligned, ld_z % 8 == 0.  A NULL / too small / misaligned ws is not an error:
+ * the launch then runs unsplit (same result, slower tail). */
 size_t cn_coatt_fused_workspace_bytes(int B, int HW, int ndir);
 int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
                           const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,

@@ -2,7 +2,7 @@
 
 Run in the build container only (it imports /root/reference, which never ships):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [nref | train473]
 
 Weights come from cosnet_amd.init_recipe (name-keyed, deterministic), inputs from
 cosnet_amd.init_recipe.synthetic_inputs (seeded).  Every fixture also carries the same
@@ -188,10 +188,52 @@ def make_nref():
     print("wrote nref5_473.npz", os.path.getsize(os.path.join(HERE, "nref5_473.npz")) // 1024, "KiB")
 
 
+def make_train473():
+    """BASELINE configs[1] pinned to the reference itself: one train step (forward of both
+    frames x both modalities, loss, backward) at 473x473 with 4 frame pairs, in fp32 and fp64
+    (rgbd_segmentation_RAA.py:139-268, train.py:595-599).  The inputs are the bench's own
+    (synthetic_inputs(4, 473, 473, seed=1234), pinned by CRC); outputs are stored on a
+    stride-2 pixel grid (the noise floors are over the full tensors), encoder features on a
+    channel / pixel subgrid, every parameter's gradient norm, the SELECT gradient heads and
+    BN buffers after the step."""
+    n, size = 4, 473
+    inp = synthetic_inputs(n, size, size, seed=1234)
+    f32, gkeys = run_train(torch.float32, inp)
+    f64, _ = run_train(torch.float64, inp)
+    arr = {"in_crc32": np.array([zlib.crc32(t.numpy().tobytes()) for t in inp], dtype=np.int64)}
+    sub = {"x1": (slice(None), slice(None), slice(None, None, 2), slice(None, None, 2)),
+           "x2": (slice(None), slice(None), slice(None, None, 2), slice(None, None, 2)),
+           "labels": (slice(None), slice(None), slice(None, None, 2), slice(None, None, 2)),
+           "V_a": (slice(None), slice(None, None, 8), slice(None, None, 3), slice(None, None, 3)),
+           "D_a": (slice(None), slice(None, None, 8), slice(None, None, 3), slice(None, None, 3))}
+    for k, v in f32.items():
+        if k in ("V_b", "D_b"):
+            continue
+        if k in sub:
+            arr["floor/" + k] = np.array([np.abs(v - f64[k]).max()])
+            arr["f32/" + k] = v[sub[k]]
+            arr["f64r/" + k] = f64[k][sub[k]]     # fp64 result, stored rounded to fp32
+            arr["f64/mean/" + k] = np.array([f64[k].mean()])
+            continue
+        put(arr, k, v, f64[k])
+    save("train_b4_473.npz", arr)
+    meta_p = os.path.join(HERE, "meta.json")
+    with open(meta_p) as f:
+        meta = json.load(f)
+    meta["train_b4_473"] = {"grad_norm_keys": gkeys, "select": SELECT, "subgrid": {
+        "x1": "[:, :, ::2, ::2]", "V_a": "[:, ::8, ::3, ::3]"}}
+    with open(meta_p, "w") as f:
+        json.dump(meta, f)
+    print("updated meta.json")
+
+
 def main():
     torch.set_num_threads(os.cpu_count())
     if len(sys.argv) > 1 and sys.argv[1] == "nref":
         make_nref()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "train473":
+        make_train473()
         return
     meta = {}
     # ---- 1. train step, B=2, 97x97 -----------------------------------------------------

@@ -115,3 +115,46 @@ def test_train_then_test_cli_end_to_end(cuda, tmp_path):
     ious = [float(x) for x in re.findall(r"IOU: ([0-9.eE+-]+)==##", text)]
     assert len(ious) == 3 and len(pngs) == 2  # 2 frames + the final mean
     assert 0.0 <= ious[-1] <= 1.0 and abs(ious[-1] - np.mean(ious[:2])) < 1e-12
+
+
+def _bench_json(out):
+    import json
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_n_spawns_n_ranks():
+    """`bench.py --gpus 2` (no WORLD_SIZE: the driver's BENCH command shape) starts a child
+    torch.distributed.run with 2 ranks and relays rank 0's single JSON line
+    (reference train.py:491-496: one replica per GPU of --gpus)."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--steps", "1", "--cpu-baseline", "0",
+                        "--no-roofline", "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _bench_json(r.stdout)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2"
+    assert j["max_rank_seconds"] >= 0.02          # max over ranks: rank 1 sleeps 20 ms
+
+
+@pytest.mark.gpu
+def test_bench_gpus_2_gloo_rehearsal_on_one_device(cuda):
+    """The same spawn path with the real model: 2 ranks on the box's one device over gloo
+    (the RCCL/xGMI figure is the driver's 8-GPU run), small shape to stay short."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--steps", "2", "--warmup", "2",
+                        "--cpu-baseline", "0", "--no-roofline", "--batch", "2", "--size", "97"],
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _bench_json(r.stdout)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2"
+    assert j["config"]["global_batch"] == 4 and j["value"] > 0 and np.isfinite(j["config"]["loss"])

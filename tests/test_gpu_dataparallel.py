@@ -81,8 +81,10 @@ def test_two_rank_graph_step_keeps_ranks_in_sync(cuda, tmp_path):
     assert not torch.equal(losses0, losses1)
 
 
-def _mean_grad_worker(rank, world, port, outdir, grad_dtype):
-    """One data-parallel SGD step (eager, momentum 0, no weight decay) against the update a
+def _mean_grad_worker(rank, world, port, outdir, grad_dtype, graphed):
+    """One data-parallel SGD step (eager, or the recorded chain of graphs: forward + head,
+    one graph per encoder segment with its bucket's async all-reduce between replays, SGD;
+    momentum 0, no weight decay) against the update a
     single process computes from the MEAN of the ranks' own gradients (each rank's gradient of
     its shard's loss with the global positive count, train.py:183-192; DataParallel's reduce)."""
     sys.path.insert(0, REPO)
@@ -122,8 +124,17 @@ def _mean_grad_worker(rank, world, port, outdir, grad_dtype):
     p0 = torch.cat([dict(m.named_parameters())[k].detach().float().flatten() for k in names])
     g0, g1 = reference_param_groups(m)
     opt = SGD([g0, g1], [lr, lr], momentum=0.0, weight_decay=0.0)
-    step = TrainStep(m, opt, 2, 65, graphed=False, grad_dtype=grad_dtype)
-    step.run_batch(*ins, [lr, lr])
+    if graphed:
+        # one eager warm-up step at lr 0 (masters unchanged: momentum 0, no weight decay), then
+        # record, then ONE replay at lr: the update comes from the graphs alone
+        step = TrainStep(m, opt, 2, 65, graphed=True, grad_dtype=grad_dtype)
+        step.load(*ins)
+        opt.set_lrs([0.0, 0.0])
+        step.capture(warmup=1)
+        step([lr, lr])
+    else:
+        step = TrainStep(m, opt, 2, 65, graphed=False, grad_dtype=grad_dtype)
+        step.run_batch(*ins, [lr, lr])
     torch.cuda.synchronize()
     p1 = torch.cat([dict(m.named_parameters())[k].detach().float().flatten() for k in names])
     torch.save({"dp": ((p0 - p1) / lr).cpu(), "mean": g.cpu()}, os.path.join(outdir, "mg%d.pt" % rank))
@@ -132,11 +143,13 @@ def _mean_grad_worker(rank, world, port, outdir, grad_dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graphed", [False, True])
 @pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
-def test_two_rank_update_is_mean_of_rank_gradients(cuda, tmp_path, grad_dtype):
+def test_two_rank_update_is_mean_of_rank_gradients(cuda, tmp_path, grad_dtype, graphed):
     import torch.multiprocessing as mp
     world = 2
-    mp.spawn(_mean_grad_worker, args=(world, _free_port(), str(tmp_path), grad_dtype), nprocs=world,
+    mp.spawn(_mean_grad_worker, args=(world, _free_port(), str(tmp_path), grad_dtype, graphed),
+             nprocs=world,
              join=True)
     for r in range(world):
         d = torch.load(os.path.join(str(tmp_path), "mg%d.pt" % r), weights_only=True)
