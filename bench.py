@@ -413,6 +413,7 @@ def main():
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if prof and dtype == torch.bfloat16 and S == 473:
         out["roofline_coattention"] = coattention_roofline(dev)
+    out["build"] = __import__("cosnet_amd._native", fromlist=["build_info"]).build_info()
     if rank == 0 and args.cpu_baseline and world == 1:
         log("cpu baseline ...")
         try:

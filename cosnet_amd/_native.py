@@ -95,6 +95,7 @@ _SIGS = {
     "cn_rowdot": (_I, [_I, _P, _L, _P, _L, _I, _I, _P, _P]),
     "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P, _P]),
     "cn_cast2d": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _I, _P]),
+    "cn_build_source_hash": (ctypes.c_char_p, []),
 }
 
 _lib = None
@@ -118,6 +119,32 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+HASHED_SOURCES = ["gemm.hip", "conv.hip", "bn.hip", "ew.hip", "coatt.hip", "coatt_fused.hip",
+                  "coatt_flash.hip", "fp8.hip", "frames.hip", "eval.hip", "common.h", "gemm.h",
+                  "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
+
+
+def source_hash():
+    """SHA-256 (16 hex digits) of the HIP sources in this tree, as the Makefile stamps it."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in HASHED_SOURCES:
+        with open(os.path.join(_HERE, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info():
+    """{library hash stamped at build, this tree's source hash, match, library sha256}."""
+    import hashlib
+    lib_hash = load().cn_build_source_hash().decode()
+    with open(LIB_PATH, "rb") as fh:
+        so = hashlib.sha256(fh.read()).hexdigest()[:16]
+    src = source_hash()
+    return {"lib_source_hash": lib_hash, "tree_source_hash": src, "built_from_tree": lib_hash == src,
+            "lib_sha256": so, "lib": os.path.relpath(LIB_PATH, os.path.dirname(_HERE))}
 
 
 def exported_symbols():

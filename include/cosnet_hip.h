@@ -308,6 +308,10 @@ int cn_frame_resize(int src_u8, const void* src, int C, long long plane_stride, 
                     long long col_stride, int y0, int x0, int h, int w, const float* mean,
                     float* dst, int H, int W, int mode, int flip, hipStream_t stream);
 
+/* Build provenance: SHA-256 (16 hex digits) of the HIP sources + this header the library was
+ * compiled from (stamped by csrc/Makefile). */
+const char* cn_build_source_hash(void);
+
 /* Development hook (tuning tools only): force GEMM tile configuration `cfg` for every bf16
  * launch; -1 restores the shape heuristic.  Returns the number of configurations. */
 int cn_gemm_force_config(int cfg);

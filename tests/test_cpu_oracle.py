@@ -143,11 +143,19 @@ def test_library_exports_every_header_symbol():
         __graft_entry__.build()
     lib = ctypes.CDLL(_native.LIB_PATH)
     hdr = open(os.path.join(REPO, "include", "cosnet_hip.h")).read()
-    names = set(re.findall(r"^(?:int|size_t)\s+(cn_\w+)\(", hdr, re.M))
+    names = set(re.findall(r"^(?:int|size_t|const char\*)\s+(cn_\w+)\(", hdr, re.M))
     assert len(names) >= 30
     for n in sorted(names):
         assert hasattr(lib, n), n
     assert names == set(_native.exported_symbols())
+
+
+def test_library_built_from_this_tree():
+    """Build provenance: the source hash stamped into the library equals the hash of the HIP
+    sources in this tree (a stale .so fails here; build() rebuilds it)."""
+    from cosnet_amd import _native
+    info = _native.build_info()
+    assert info["built_from_tree"], info
 
 
 def test_forward_requires_gpu_no_cpu_fallback(model_cpu):

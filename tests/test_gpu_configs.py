@@ -116,13 +116,43 @@ def test_coattfn_parameter_weight_no_grad_is_fused(cuda, monkeypatch):
     assert calls == [1] and za.requires_grad
 
 
+class _RoundBF16(torch.autograd.Function):
+    """bf16 storage point of the HIP path: rounds the value and the gradient through it."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).double()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).double()
+
+
+def _coatt_ref(va, vb, w, emul):
+    """rgbd_segmentation_RAA.py:150-170 in fp64 (oracle.model_ref.RefModel.coattention's op
+    sequence); emul=True rounds V_a W^T to bf16 where the bf16 HIP path stores it."""
+    import torch.nn.functional as Fn
+    n, c, h, wd = va.shape
+    va_f, vb_f = va.reshape(n, c, h * wd), vb.reshape(n, c, h * wd)
+    va_t = Fn.linear(va_f.transpose(1, 2), w)
+    if emul:
+        va_t = _RoundBF16.apply(va_t)
+    s = torch.bmm(va_t, vb_f)
+    z_b = torch.bmm(va_f, Fn.softmax(s, dim=1))
+    z_a = torch.bmm(vb_f, Fn.softmax(s.transpose(1, 2), dim=1))
+    return z_a.reshape(n, c, h, wd), z_b.reshape(n, c, h, wd)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_coattention_block_hw3600_b4(cuda, dt):
     """CoattFn forward AND backward at the configs[1] training shape (B = 4 pairs, 60 x 60
-    features, C = 256, S of 3600 x 3600 per pair) against the oracle in fp64 (computed on the
-    device: test arithmetic, not the product path).  Logits std ~16 as in the model.
-    fp32 2e-4 of the output scale; bf16 0.15 (P and V_a W^T rounded to bf16, SURVEY §7 iii)."""
-    from oracle.model_ref import RefModel
+    features, C = 256, S of 3600 x 3600 per pair) against the reference op sequence in fp64
+    (computed on the device: test arithmetic, not the product path).  Logits std ~16 as in the
+    model.  fp32: 2e-4 of the output scale.  bf16: 3e-2 of the output scale (the bound the flash
+    kernels meet in tests/test_gpu_coatt_fused.py) against fp64 with V_a W^T rounded to bf16
+    where the HIP path stores it, and no further from pure fp64 than that rounding itself puts
+    it (<= 1.25 x its own distance + 2e-3): at logits of std 16 one bf16 rounding of V_a W^T moves
+    S by ~0.05, i.e. P by ~5 %, for ANY bf16 implementation (measured 3.3e-2 vs pure fp64)."""
     from cosnet_amd.functions import CoattFn
     n, c, h, w = 4, 256, 60, 60
     gen = torch.Generator().manual_seed(36)
@@ -133,10 +163,13 @@ def test_coattention_block_hw3600_b4(cuda, dt):
     va, vb = rnd((n, c, h, w)), rnd((n, c, h, w))
     W = rnd((c, c), c ** -0.5).float().double()
     gza, gzb = rnd((n, c, h, w)), rnd((n, c, h, w))
-    var = va.to(cuda).requires_grad_(True)
-    wr = W.to(cuda).requires_grad_(True)
-    za, zb = RefModel.coattention(None, var, vb.to(cuda), wr)
-    ((za * gza.to(cuda)).sum() + (zb * gzb.to(cuda)).sum()).backward()
+    refs = {}
+    for emul in ((False, True) if dt == torch.bfloat16 else (False,)):
+        var = va.to(cuda).requires_grad_(True)
+        wr = W.to(cuda).requires_grad_(True)
+        za, zb = _coatt_ref(var, vb.to(cuda), wr, emul)
+        ((za * gza.to(cuda)).sum() + (zb * gzb.to(cuda)).sum()).backward()
+        refs[emul] = {"Z_a": za.detach(), "Z_b": zb.detach(), "dV_a": var.grad, "dW": wr.grad}
     nhwc = lambda x: x.permute(0, 2, 3, 1).reshape(n * h * w, c)
     vag = nhwc(va).to(dt).to(cuda).contiguous().requires_grad_(True)
     vbg = nhwc(vb).to(dt).to(cuda).contiguous()
@@ -144,13 +177,93 @@ def test_coattention_block_hw3600_b4(cuda, dt):
     ga, gb = CoattFn.apply(vag, vbg, Wg, (n, h * w))
     torch.autograd.backward([ga, gb], [nhwc(gza).to(dt).to(cuda), nhwc(gzb).to(dt).to(cuda)])
     torch.cuda.synchronize()
-    tol = {torch.float32: 2e-4, torch.bfloat16: 0.15}[dt]
     nchw = lambda t: t.reshape(n, h, w, c).permute(0, 3, 1, 2)
-    for name, got, ref in (("Z_a", nchw(ga), za), ("Z_b", nchw(gb), zb),
-                           ("dV_a", nchw(vag.grad), var.grad), ("dW", Wg.grad, wr.grad)):
-        got, ref = got.double(), ref.detach().double()
-        err = ((got - ref).abs().max() / ref.abs().max()).item()
-        assert err <= tol, (name, err, tol)
+    got = {"Z_a": nchw(ga), "Z_b": nchw(gb), "dV_a": nchw(vag.grad), "dW": Wg.grad}
+    rel = lambda a, b: ((a.double() - b.double()).abs().max() / b.double().abs().max()).item()
+    for name in got:
+        if dt == torch.float32:
+            err = rel(got[name], refs[False][name])
+            assert err <= 2e-4, (name, err)
+        else:
+            e_em, e_pure = rel(got[name], refs[True][name]), rel(got[name], refs[False][name])
+            floor = rel(refs[True][name], refs[False][name])
+            print("%s bf16: vs emul %.2e, vs pure %.2e, floor %.2e" % (name, e_em, e_pure, floor))
+            assert e_em <= 3e-2 and e_pure <= 1.25 * floor + 2e-3, (name, e_em, e_pure, floor)
+
+
+def test_configs1_473_b4_fp32_matches_reference(cuda):
+    """configs[1] pinned to the REFERENCE itself: one fp32 train step (forward of both frames x
+    both modalities, loss, backward) at 473 x 473 with 4 frame pairs, against the reference run
+    in fp64 on the same inputs / weights (tests/golden/train_b4_473.npz, make_golden.py train473;
+    rgbd_segmentation_RAA.py:139-268, train.py:595-599).  Floor rule of tests/test_gpu_model.py:
+    outputs within 8x the reference's own fp32-vs-fp64 floor, masks identical outside the
+    ambiguity band, gradient norms within max(8x own floor, p90 floor), gradient heads and BN
+    buffers within 8x floor.  Outputs / features are compared on the fixture's subgrid."""
+    from conftest import golden_meta
+    z = golden("train_b4_473.npz")
+    meta = golden_meta()["train_b4_473"]
+    inp = synthetic_inputs(4, 473, 473, seed=1234)
+    assert [zlib.crc32(t.numpy().tobytes()) for t in inp] == list(z["in_crc32"]), \
+        "synthetic input generator drifted"
+    inp = [t.to(cuda) for t in inp]
+    m = make_model(cuda, torch.float32).train()
+    stages = {}
+    x1, x2, labels = m(*inp[:4], stages=stages)
+    loss = L.bce_l1(x1, inp[4]) + L.bce_l1(x2, inp[5])
+    loss.backward()
+    torch.cuda.synchronize()
+    n, h, w = stages["geo"]
+    to_nchw = lambda t: t.float().view(n, h, w, -1).permute(0, 3, 1, 2)
+    sub2 = (slice(None), slice(None), slice(None, None, 2), slice(None, None, 2))
+    subf = (slice(None), slice(None, None, 8), slice(None, None, 3), slice(None, None, 3))
+    for name, t, sub in (("x1", x1, sub2), ("x2", x2, sub2), ("labels", labels, sub2),
+                         ("V_a", to_nchw(stages["V_a"]), subf), ("D_a", to_nchw(stages["D_a"]), subf)):
+        ref = z["f64r/" + name].astype(np.float64)
+        got = t.detach().double()[sub].cpu().numpy()
+        floor = float(z["floor/" + name][0])
+        tol = 8 * floor + 1e-5 * max(1.0, float(np.abs(ref).max()))
+        err = float(np.abs(got - ref).max())
+        assert err <= tol, "%s: max err %.3g > tol %.3g (floor %.3g)" % (name, err, tol, floor)
+        if name in ("x1", "x2"):
+            amb = np.abs(ref - 0.5) <= tol
+            flips = ((got > 0.5) != (ref > 0.5)) & ~amb
+            assert not flips.any(), (name, int(flips.sum()))
+            full_mean = float(z["f64/mean/" + name][0])
+            assert abs(t.double().mean().item() - full_mean) <= tol, name
+    lref, lfloor = float(z["f64/loss"][0]), float(z["floor/loss"][0])
+    assert abs(loss.item() - lref) <= 8 * lfloor + 1e-5 * abs(lref), (loss.item(), lref, lfloor)
+    named = dict(m.named_parameters())
+    norms = np.array([named[k].grad.double().norm().item() for k in meta["grad_norm_keys"]])
+    ref = z["f64/grad_norm"]
+    rel = np.abs(norms - ref) / np.maximum(ref, 1e-12)
+    floor = np.abs(z["f32/grad_norm"] - ref) / np.maximum(ref, 1e-12)
+    zero = ref < 1e-6 * np.median(ref)   # analytically zero (conv bias before a train-mode BN)
+    # per tensor: 8x its own reference floor or the 99th percentile of the reference's floors
+    # (a tensor whose reference fp32 error happens to be tiny is not held to that luck); and the
+    # error DISTRIBUTION within 1.5x the reference's own fp32 one
+    nz = ~zero
+    tol = np.maximum(8 * floor, np.quantile(floor[nz], 0.99)) + 1e-3
+    ok = (rel <= tol) | (zero & (norms < 1e-5 * np.median(ref)))
+    for q in (0.5, 0.9):
+        assert np.quantile(rel[nz], q) <= 1.5 * np.quantile(floor[nz], q) + 1e-4, q
+    print("configs[1] fp32 grad-norm rel err vs fp64: median %.2e p90 %.2e max %.2e; reference's own "
+          "fp32 floor: median %.2e p90 %.2e max %.2e" % (
+              np.median(rel[nz]), np.quantile(rel[nz], 0.9), rel[nz].max(), np.median(floor[nz]),
+              np.quantile(floor[nz], 0.9), floor[nz].max()))
+    assert ok.all(), "grad norms off: %s" % [(meta["grad_norm_keys"][i], "%.2e" % rel[i], "%.2e" % tol[i])
+                                              for i in np.nonzero(~ok)[0]][:8]
+    for k in meta["select"]:
+        g = named[k].grad.detach().double().flatten().cpu().numpy()
+        r = z["f64/grad_head/" + k]
+        fl = float(z["floor/grad_head/" + k][0])
+        err = np.abs(g[:r.size] - r).max()
+        assert err <= 8 * fl + 0.02 * np.abs(r).max(), (k, err, fl)
+    sd = m.state_dict()
+    for k in [f for f in z.files if f.startswith("f64/buf/")]:
+        key = k[len("f64/buf/"):]
+        got = sd[key].double().cpu().numpy()
+        fl = float(z["floor/buf/" + key][0])
+        assert np.abs(got - z[k]).max() <= 8 * fl + 1e-6 * max(1.0, np.abs(z[k]).max()), key
 
 
 def _step_once(m, inp):
@@ -165,8 +278,9 @@ def _grad_norms(m):
 
 def test_configs1_473_b4_bf16_step_tracks_fp32(cuda):
     """configs[1]: 473 x 473, 4 frame pairs, bf16, fwd + loss + bwd on the HIP path, with the
-    same inputs / weights through the fp32 HIP path as the yardstick (the oracle cannot run this
-    size in a test's time budget; the fp32 path itself is pinned to the reference fixtures).
+    same inputs / weights through the fp32 HIP path as the yardstick (the fp32 path itself is
+    pinned to the reference at this very configuration by the test above; bf16 blocks are pinned
+    to fp64 in tests/test_gpu_blocks_bf16.py).
     The random-init 101-layer network is chaotic in bf16 (pixel masks decorrelate: measured 85 %
     agreement with fp32 outside |x - 0.5| <= 0.05), so the comparison is on the aggregates a
     training step consumes: finite loss and gradients; |loss_bf16 - loss_fp32| <= 3 % of

@@ -68,6 +68,10 @@ def get_arguments(argv=None):
                    help="data-parallel gradient reduction dtype (bucketed, overlapped)")
     p.add_argument("--log-mem", type=int, default=1,
                    help="logMem lines around each iteration like train.py:560-621 (0: off)")
+    p.add_argument("--gc-every-iter", type=int, default=0,
+                   help="1: gc.collect() + torch.cuda.empty_cache() after every iteration as the "
+                        "reference does (train.py:619-620); off by default: it costs host time "
+                        "and can release pool memory a recorded step graph relies on")
     return p.parse_args(argv)
 
 
@@ -325,8 +329,9 @@ def main(argv=None):
                     epoch, i_iter, train_len, lv, lr))
                 logger.flush()
             del batch, ins
-            gc.collect()
-            torch.cuda.empty_cache()
+            if args.gc_every_iter:
+                gc.collect()
+                torch.cuda.empty_cache()
             mem(" After GC")
         step.sync_buffers()  # rank 0's BN buffers, like DataParallel's replica 0
         if is0:
