@@ -2,7 +2,9 @@
 #pragma once
 #include "common.h"
 
-enum LoadKind { L_KC_DENSE = 0, L_KC_CONV = 1, L_MC_DENSE = 2, L_MC_CONV = 3 };
+enum LoadKind { L_KC_DENSE = 0, L_KC_CONV = 1, L_MC_DENSE = 2, L_MC_CONV = 3,
+                L_KC_CONV_G = 4 };   // KC_CONV whose K tiles may straddle taps (C % BK != 0);
+                                     // picked by cn_gemm_dispatch, callers pass L_KC_CONV
 
 // Gather geometry.  For a KC_CONV A operand the GEMM row m is an output pixel (n, oy, ox)
 // over the (OH, OW) grid and k = (r, s, ci); the source element is

@@ -42,12 +42,35 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// Buffer-descriptor form of the same LDS-DMA (buffer_load_dwordx4 ... lds): address = base +
+// soffset (SGPR, wave-uniform: the K position of the tile) + voffset (VGPR, constant per chunk
+// over a whole tap / the whole K loop).  The hardware range check covers voffset only (not
+// soffset): a chunk with no source (padding row / column, conv tap outside the image, k past the
+// end) gets voffset = BUF_OOB and reads zeros -- no zero page, no per-chunk select, no 64-bit
+// address arithmetic in the K loop.
+constexpr unsigned BUF_OOB = 0x80000000u;   // = num_records of every operand descriptor
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)BUF_OOB, 0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff,
+                                       char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base,
+                                           16, (int)voff, (int)soff, 0, 0);
+}
+
 // -------------------------------------------------------------------------------------
-// Operand loader: LDS-DMA (global_load_lds_dwordx4) fill of one ROWS x 128-byte K tile per
-// call, NCH = ROWS*8/NT 16-byte chunks per thread.  Everything that does not change along K
-// (row / column pointers, the conv gather's per-chunk tap offsets, pixel coordinates) is
-// computed once in init(); issue() then costs a few VALU per chunk and advances the state by
-// one K tile (tiles are issued strictly in order, starting at kbeg).
+// Operand loader: LDS-DMA fill of one ROWS x 128-byte K tile per call, NCH = ROWS*8/NT 16-byte
+// chunks per thread.  Everything that does not change along K is computed once in init().
+//
+// KC_DENSE, KC_CONV (C % BK == 0) and MC_DENSE use the buffer-descriptor DMA (blds16): each
+// chunk keeps a 32-bit byte offset that is constant over the whole K loop (KC_DENSE, MC_DENSE)
+// or over one conv tap (KC_CONV), and the K position of the tile goes into the wave-uniform
+// soffset -- so a K step costs no vector address arithmetic at all: the tap and channel base of
+// a tile are scalars (a K tile never straddles taps when C % BK == 0) and a missing source
+// (padding row, tap outside the image, k past the end) is the out-of-range offset BUF_OOB,
+// which the hardware reads as zeros.  KC_CONV_G (conv gathers with C % BK != 0: the stems,
+// fp8 on 64-channel layers) and MC_CONV (weight-gradient B operand) keep per-thread pointers and
+// the flat global_load_lds.  Tiles are issued strictly in order, starting at kbeg.
 // -------------------------------------------------------------------------------------
 template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr int VEC = VecOf<T>::N;
@@ -56,21 +79,26 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr int RSTEP = NT / 8;            // KC: rows between a thread's chunks
   static_assert(NCH >= 1 && NCH * NT == ROWS * 8, "tile rows must fill whole chunk rounds");
   static constexpr bool MC = (KIND == L_MC_DENSE || KIND == L_MC_CONV);
+  static constexpr bool BUF = (KIND == L_KC_DENSE || KIND == L_KC_CONV || KIND == L_MC_DENSE);
   static constexpr int CPR = ROWS / VEC;          // MC: chunks per k-row
   static constexpr int KROW_STEP = NT / CPR;      // MC: k-rows between a thread's chunks
   static constexpr int RB = ROWS * (int)sizeof(T);  // MC: bytes per k-row of the LDS image
+  static constexpr unsigned SZ = sizeof(T);
 
-  const T* base;
   long long ld;
   int klim;             // k bound (zero beyond)
+  int kbeg;
   int kcol;             // KC: this thread's k offset within a tile (swizzled chunk * VEC)
-  const T* ptr[NCH];    // KC_DENSE: row pointer + kcol; MC_DENSE: next k-row pointer;
-                        // KC_CONV: pixel pointer of the cached tap (+ kcol)
   bool ok[NCH];         // row / column / pixel validity
-  // KC_CONV
+  // buffer path
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned voff[NCH];   // byte offset of chunk i (BUF_OOB: no source)
+  // KC_CONV / KC_CONV_G
   int img[NCH], by[NCH], bx[NCH];
-  int ctap;             // tap whose pixel pointers are cached (-1: none)
-  bool tap_uniform;     // C % BK == 0: a K tile never straddles two taps
+  int ctap;             // tap whose offsets / pointers are cached (-1: none)
+  // flat path (KC_CONV_G, MC_CONV)
+  const T* base;
+  const T* ptr[NCH];    // KC_CONV_G: pixel pointer of the cached tap
   // MC_CONV: per-chunk column (tap offsets, channel) and output-pixel coordinates
   int ry[NCH], sx[NCH], cic[NCH];
   int pim[NCH], poy[NCH], pox[NCH], pp[NCH];
@@ -78,18 +106,22 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
   ConvGeom g;
 
   __device__ __forceinline__ void init(const T* b, long long ld_, int lim, int klim_,
-                                       const ConvGeom& geo, int origin, int tid, int kbeg) {
-    base = b; ld = ld_; klim = klim_;
+                                       const ConvGeom& geo, int origin, int tid, int kbeg_) {
+    ld = ld_; klim = klim_; kbeg = kbeg_;
+    base = b;
     if (!MC) {
       const int pos = tid & 7;
       kcol = (pos ^ ((tid >> 3) & 7)) * VEC;  // row & 7 == (tid >> 3) & 7 for every chunk
+      if (KIND == L_KC_DENSE) rsrc = buf_rsrc(b + (long long)origin * ld);   // block-rebased
+      if (KIND == L_KC_CONV) rsrc = buf_rsrc(b);
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        const int row = origin + (tid >> 3) + RSTEP * i;
+        const int rl = (tid >> 3) + RSTEP * i;   // row within the tile
+        const int row = origin + rl;
         ok[i] = row < lim;
         const int rr = ok[i] ? row : 0;
         if (KIND == L_KC_DENSE) {
-          ptr[i] = base + (long long)rr * ld + kcol;
+          voff[i] = ok[i] ? (unsigned)((rl * ld + kcol) * SZ) : BUF_OOB;
         } else {
           int q, rem, oy, ox;
           fdivmod(rr, geo.div_OHW, q, rem);
@@ -99,13 +131,13 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
           bx[i] = ox * geo.st + geo.off_x;
         }
       }
-      if (KIND == L_KC_CONV) {
+      if (KIND == L_KC_CONV || KIND == L_KC_CONV_G) {
         g = geo;
         ctap = -1;
-        tap_uniform = (geo.C % BK) == 0;
       }
     } else {
       const int pos = tid % CPR;
+      if (KIND == L_MC_DENSE) rsrc = buf_rsrc(b + (long long)kbeg_ * ld + origin);   // block-rebased
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int krl = tid / CPR + KROW_STEP * i;  // k-row within the tile
@@ -113,7 +145,7 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
         const int col = origin + cchunk * VEC;
         ok[i] = col < lim;
         if (KIND == L_MC_DENSE) {
-          ptr[i] = base + (long long)(kbeg + krl) * ld + col;
+          voff[i] = ok[i] ? (unsigned)((krl * ld + cchunk * VEC) * SZ) : BUF_OOB;
         } else {
           const int nn = ok[i] ? col : 0;
           int tap, r, s2;
@@ -121,7 +153,7 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
           fdivmod(tap, geo.div_KW, r, s2);
           ry[i] = r * geo.step_y + geo.off_y;
           sx[i] = s2 * geo.step_x + geo.off_x;
-          pp[i] = kbeg + krl;
+          pp[i] = kbeg_ + krl;
           int q, rem, oy, ox;
           fdivmod(pp[i] < klim ? pp[i] : 0, geo.div_OHW, q, rem);
           fdivmod(rem, geo.div_OW, oy, ox);
@@ -138,23 +170,64 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
     }
   }
 
-  // LDS-DMA fill: chunk q = tid + NT i lands at byte 16 q of the tile (lane-linear per wave
-  // instruction); the XOR swizzle lives in the SOURCE address so the image is the swizzled
-  // layout the fragment readers expect.  Out-of-bounds chunks read the zero page.
+  // Fill of one K tile: chunk q = tid + NT i lands at byte 16 q of the tile (lane-linear per
+  // wave instruction); the XOR swizzle lives in the SOURCE address so the image is the swizzled
+  // layout the fragment readers expect.
   __device__ __forceinline__ void issue(int k0, char* lds, int tid) {
-    const void* zp = (const void*)g_zero16;
-    char* wbase = lds + (tid & ~63) * 16;
-    if (KIND == L_KC_DENSE) {
-      const bool kok = k0 + kcol < klim;
+    char* wbase = lds + __builtin_amdgcn_readfirstlane((tid & ~63) * 16);
+    // k0 is wave-uniform: whole-tile bounds and the tap / offset arithmetic below are scalar
+    const bool tail = k0 + BK > klim;
+    if constexpr (KIND == L_KC_DENSE) {
+      if (!tail) {
 #pragma unroll
-      for (int i = 0; i < NCH; ++i)
-        glds16((ok[i] && kok) ? (const void*)(ptr[i] + k0) : zp, wbase + i * NT * 16);
-    } else if (KIND == L_KC_CONV) {
+        for (int i = 0; i < NCH; ++i) blds16(rsrc, voff[i], (unsigned)k0 * SZ, wbase + i * NT * 16);
+      } else {
+        const bool kok = k0 + kcol < klim;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) blds16(rsrc, kok ? voff[i] : BUF_OOB, (unsigned)k0 * SZ, wbase + i * NT * 16);
+      }
+    } else if constexpr (KIND == L_KC_CONV) {
+      const int tap = __builtin_amdgcn_readfirstlane(fdiv(k0, g.div_C));
+      if (tap != ctap) {   // new tap (uniform branch): the chunks' pixel offsets
+        int r, ss;
+        fdivmod(tap, g.div_KW, r, ss);
+        const int oy = r * g.step_y, ox = ss * g.step_x;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          const int y = by[i] + oy, x = bx[i] + ox;
+          const bool v = img[i] >= 0 && (unsigned)y < (unsigned)g.H && (unsigned)x < (unsigned)g.W;
+          const unsigned pix = (unsigned)((img[i] * g.H + y) * g.W + x);
+          voff[i] = v ? (pix * (unsigned)ld + (unsigned)kcol) * SZ : BUF_OOB;
+        }
+        ctap = tap;
+      }
+      const unsigned soff = (unsigned)(k0 - tap * g.C) * SZ;
+      if (!tail) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) blds16(rsrc, voff[i], soff, wbase + i * NT * 16);
+      } else {
+        const bool kok = k0 + kcol < klim;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) blds16(rsrc, kok ? voff[i] : BUF_OOB, soff, wbase + i * NT * 16);
+      }
+    } else if constexpr (KIND == L_MC_DENSE) {
+      const unsigned soff = (unsigned)(k0 - kbeg) * (unsigned)ld * SZ;
+      if (!tail) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) blds16(rsrc, voff[i], soff, wbase + i * NT * 16);
+      } else {
+        const int kr0 = k0 + tid / CPR;
+#pragma unroll
+        for (int i = 0; i < NCH; ++i)
+          blds16(rsrc, kr0 + KROW_STEP * i < klim ? voff[i] : BUF_OOB, soff, wbase + i * NT * 16);
+      }
+    } else if constexpr (KIND == L_KC_CONV_G) {
+      const void* zp = (const void*)g_zero16;
       const int k = k0 + kcol;
       const bool kok = k < klim;
       int tap, cc;
       fdivmod(kok ? k : 0, g.div_C, tap, cc);
-      if (!tap_uniform || tap != ctap) {  // new tap: recompute the pixel pointers
+      if (tap != ctap) {  // new tap: recompute the pixel pointers
         int r, ss;
         fdivmod(tap, g.div_KW, r, ss);
         const int oy = r * g.step_y, ox = ss * g.step_x;
@@ -171,15 +244,8 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
 #pragma unroll
       for (int i = 0; i < NCH; ++i)
         glds16((ok[i] && kok) ? (const void*)(ptr[i] + cc) : zp, wbase + i * NT * 16);
-    } else if (KIND == L_MC_DENSE) {
-      const int kr0 = k0 + tid / CPR;
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) {
-        const bool v = ok[i] && kr0 + KROW_STEP * i < klim;
-        glds16(v ? (const void*)ptr[i] : zp, wbase + i * NT * 16);
-        ptr[i] += (long long)BK * ld;
-      }
     } else {  // L_MC_CONV: k = output pixel, n = (tap, ci) fixed per chunk
+      const void* zp = (const void*)g_zero16;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int y = poy[i] * g.st + ry[i], x = pox[i] * g.st + sx[i];
@@ -845,10 +911,26 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
   }
 }
 
+// conv gathers whose K tiles straddle taps (C % BK != 0: the 8-channel padded stems): the
+// tiles the heuristic picks for those shapes only
+template <class T, class CT>
+static int launch_conv_g(const GemmArgs& a, int batch, hipStream_t st) {
+  if constexpr (sizeof(T) == 4) {
+    if (a.N <= 64 || cfg_blocks(1, a, batch) < 384) return launch_c<T, CT, 0, L_KC_CONV_G, L_KC_DENSE>(a, batch, st);
+    return launch_c<T, CT, 1, L_KC_CONV_G, L_KC_DENSE>(a, batch, st);
+  } else {
+    const int c = pick_cfg(a, batch);
+    if (c == 12) return launch_c<T, CT, 12, L_KC_CONV_G, L_KC_DENSE>(a, batch, st);
+    if (c == 13) return launch_c<T, CT, 13, L_KC_CONV_G, L_KC_DENSE>(a, batch, st);
+    return launch_c<T, CT, 11, L_KC_CONV_G, L_KC_DENSE>(a, batch, st);
+  }
+}
+
 template <class T, class CT>
 static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_t st) {
 #define CN_CASE(A_, B_) \
   if (la == A_ && lb == B_) return launch_tile<T, CT, A_, B_>(a, batch, st);
+  if (la == L_KC_CONV_G && lb == L_KC_DENSE) return launch_conv_g<T, CT>(a, batch, st);
   CN_CASE(L_KC_DENSE, L_KC_DENSE)
   CN_CASE(L_KC_CONV, L_KC_DENSE)
   CN_CASE(L_KC_DENSE, L_MC_DENSE)
@@ -869,20 +951,39 @@ static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
   return launch_c<f8e4m3, CT, 11, LA, L_KC_DENSE>(a, batch, st);
 }
 
+// 32-bit byte-offset limits of the buffer-descriptor loaders (Loader, BUF path)
+static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
+  const long long ld = is_a ? a.lda : a.ldb;
+  const ConvGeom& g = is_a ? a.ga : a.gb;
+  const long long kspan = a.nsplit > 1 ? a.k_chunk : a.K;
+  if (kind == L_KC_DENSE) return 256 * ld * esz < 0x80000000ll && (long long)a.K * esz < 0xFFFF0000ll;
+  if (kind == L_KC_CONV) return (long long)g.N * g.H * g.W * ld * esz < 0x80000000ll;
+  if (kind == L_MC_DENSE) return (kspan + 128) * ld * esz < 0xFFFF0000ll && 128 * ld * esz < 0x80000000ll;
+  return true;
+}
+
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
+  const int esz = dtype == DT_FP8 ? 1 : dtype == DT_BF16 ? 2 : 4;
+  const int bk = 128 / esz;
+  // conv gathers whose K tiles can straddle taps, or too large for 32-bit offsets: per-thread
+  // pointer loader
+  if (la == L_KC_CONV && (a.ga.C % bk != 0 || !buf_ok(L_KC_CONV, a, true, esz))) la = L_KC_CONV_G;
+  if (!buf_ok(la, a, true, esz) || !buf_ok(lb, a, false, esz)) return CN_ERR_SHAPE;
   if (dtype == DT_FP8) {
     if (lb != L_KC_DENSE || a.st_mode || a.nsplit != 1) return CN_ERR_UNSUPPORTED;
     if (la == L_KC_DENSE) return c_f32 ? launch_f8<float, L_KC_DENSE>(a, batch, st) : launch_f8<bf16, L_KC_DENSE>(a, batch, st);
     if (la == L_KC_CONV) return c_f32 ? launch_f8<float, L_KC_CONV>(a, batch, st) : launch_f8<bf16, L_KC_CONV>(a, batch, st);
+    if (la == L_KC_CONV_G) return c_f32 ? launch_f8<float, L_KC_CONV_G>(a, batch, st) : launch_f8<bf16, L_KC_CONV_G>(a, batch, st);
     return CN_ERR_UNSUPPORTED;
   }
   if (a.st_mode) {
     if (batch != 1 || a.nsplit != 1 || a.row_map || a.c_mode ||
-        lb != L_KC_DENSE || (la != L_KC_DENSE && la != L_KC_CONV))
+        lb != L_KC_DENSE || (la != L_KC_DENSE && la != L_KC_CONV && la != L_KC_CONV_G))
       return CN_ERR_UNSUPPORTED;
 #define CN_EPI(T_, M_) \
-    return la == L_KC_DENSE ? launch_epi<T_, L_KC_DENSE, M_>(a, st) : launch_epi<T_, L_KC_CONV, M_>(a, st)
+    return la == L_KC_DENSE ? launch_epi<T_, L_KC_DENSE, M_>(a, st) : \
+           la == L_KC_CONV ? launch_epi<T_, L_KC_CONV, M_>(a, st) : launch_epi<T_, L_KC_CONV_G, M_>(a, st)
     if (dtype == DT_BF16) {
       if (a.st_mode == 1) CN_EPI(bf16, 1); else CN_EPI(bf16, 2);
     } else {
