@@ -30,6 +30,9 @@ _SIGS = {
     "cn_conv_wgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "cn_splitk_reduce": (_I, [_P, _I, _L, _L, _P, _I, _P]),
     "cn_fp8_quant": (_I, [_I, _P, _L, _I, _I, _P, _L, _P, _I, _P]),
+    "cn_fp8_quant_fmt": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _P, _I, _P]),
+    "cn_conv_dgrad_fp8": (_I, [_P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _L, _I, _I, _I,
+                               _P, _P, _P]),
     "cn_fp8_update": (_I, [_P, _I, _F, _P]),
     "cn_fp8_quant_multi": (_I, [_P, _I, _P]),
     "cn_conv_fwd_fp8": (_I, [_P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I, _P,

@@ -16,17 +16,19 @@ typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 // dtype codes shared with the C ABI (include/cosnet_hip.h)
-enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
+enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2, DT_FP8_E5M2 = 3 };  // DT_FP8_E5M2 GEMM: A e5m2, B e4m3
 
 // OCP fp8 e4m3 (gfx950's e4m3fn, not MI300's fnuz), stored as raw bytes; matrix-core operand
 // only (the fp8 GEMMs read it, elementwise code never computes in it)
 struct f8e4m3 { unsigned char v; };
+struct f8e5m2 { unsigned char v; };   // OCP e5m2 ("bf8"): gradients
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 template <class T> struct VecOf;
 template <> struct VecOf<float> { static constexpr int N = 4; };  // elements per 16-byte chunk
 template <> struct VecOf<bf16> { static constexpr int N = 8; };
 template <> struct VecOf<f8e4m3> { static constexpr int N = 16; };
+template <> struct VecOf<f8e5m2> { static constexpr int N = 16; };
 
 __device__ __forceinline__ float tof(float x) { return x; }
 __device__ __forceinline__ float tof(bf16 x) { return (float)x; }

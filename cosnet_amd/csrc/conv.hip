@@ -102,6 +102,33 @@ extern "C" int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int 
   return cn_gemm_dispatch(a, DT_FP8, 0, la, L_KC_DENSE, 1, st);
 }
 
+// dx (bf16) (+)= conv_dgrad(dy8, wt8) * dy_scale * w_scale, stride 1: e5m2 output gradients
+// (delayed scaling, cn_fp8_quant_fmt) x e4m3 transposed weights [Cin][KH][KW][Cout] on the
+// block-scaled 16x16x128 MFMA (A format e5m2, B e4m3), fp32 accumulation.
+extern "C" int cn_conv_dgrad_fp8(const void* dy8, long long lddy, int N, int OH, int OW, int Cout,
+                                 const void* wt8, int Cin, int KH, int KW, int pad, int dil,
+                                 void* dx, long long lddx, int H, int W, int accumulate,
+                                 const float* dy_state, const float* w_state, hipStream_t st) {
+  if (Cout % 16 || lddy % 16 || ((uintptr_t)dy8 & 15) || ((uintptr_t)wt8 & 15)) return CN_ERR_ALIGN;
+  if (lddx % 8 || ((uintptr_t)dx & 15)) return CN_ERR_ALIGN;
+  if (OH != H + 2 * pad - dil * (KH - 1) || OW != W + 2 * pad - dil * (KW - 1)) return CN_ERR_SHAPE;
+  GemmArgs a = gemm_defaults();
+  a.M = N * H * W; a.N = Cin; a.K = KH * KW * Cout;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = dy8; a.lda = lddy;
+  a.B = wt8; a.ldb = a.K;
+  a.C = dx; a.ldc = lddx;
+  a.c_mode = accumulate ? 2 : 0;
+  a.scale_a = dy_state;
+  a.scale_b = w_state;
+  int la = L_KC_DENSE;
+  if (!(KH == 1 && KW == 1 && pad == 0)) {
+    la = L_KC_CONV;
+    a.ga = make_geom(N, OH, OW, Cout, H, W, KH, KW, 1, pad, pad, -dil, -dil);
+  }
+  return cn_gemm_dispatch(a, DT_FP8_E5M2, 0, la, L_KC_DENSE, 1, st);
+}
+
 static long long mtiles_of(int dtype, int M, int N, int K) {
   const int bm = cn_gemm_bm(dtype, M, N, K, -1);
   return (M + bm - 1) / bm;

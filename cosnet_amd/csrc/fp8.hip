@@ -14,6 +14,8 @@ namespace {
 
 constexpr float FP8_MAX = 448.f;
 
+constexpr float BF8_MAX = 57344.f;   // OCP e5m2 max finite (gradients)
+
 __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
   a = fminf(fmaxf(a, -FP8_MAX), FP8_MAX);
   b = fminf(fmaxf(b, -FP8_MAX), FP8_MAX);
@@ -21,6 +23,18 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   d = fminf(fmaxf(d, -FP8_MAX), FP8_MAX);
   unsigned w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
   return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+__device__ __forceinline__ unsigned pack4_bf8(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -BF8_MAX), BF8_MAX);
+  b = fminf(fmaxf(b, -BF8_MAX), BF8_MAX);
+  c = fminf(fmaxf(c, -BF8_MAX), BF8_MAX);
+  d = fminf(fmaxf(d, -BF8_MAX), BF8_MAX);
+  unsigned w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+}
+template <int FMT>
+__device__ __forceinline__ unsigned pack4(float a, float b, float c, float d) {
+  return FMT ? pack4_bf8(a, b, c, d) : pack4_fp8(a, b, c, d);
 }
 
 // block max -> ONE atomic per block (same-address atomics serialise in L2)
@@ -40,7 +54,7 @@ __device__ __forceinline__ void wave_amax_atomic(float m, float* state) {
 // y8[r][c] = fp8(x[r][c] * state[1]) for a [P][C] matrix (row strides ldx / ldy, C % 8 == 0);
 // amax of |x| accumulated into state[2] when `collect`.  Block = 64 chunk-columns (8 elements
 // each) x 4 row groups; rows strided over gridDim.y -- no index division in the loop.
-template <class T>
+template <class T, int FMT>
 __global__ __launch_bounds__(256) void quant_fp8_k(const T* __restrict__ x, long long ldx, int P, int C,
                                                    unsigned char* __restrict__ y, long long ldy,
                                                    float* state, int quantise, int collect) {
@@ -72,8 +86,8 @@ __global__ __launch_bounds__(256) void quant_fp8_k(const T* __restrict__ x, long
         for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[u][e]));
         if (quantise) {
           u32x2 o;
-          o.x = pack4_fp8(f[u][0] * inv, f[u][1] * inv, f[u][2] * inv, f[u][3] * inv);
-          o.y = pack4_fp8(f[u][4] * inv, f[u][5] * inv, f[u][6] * inv, f[u][7] * inv);
+          o.x = pack4<FMT>(f[u][0] * inv, f[u][1] * inv, f[u][2] * inv, f[u][3] * inv);
+          o.y = pack4<FMT>(f[u][4] * inv, f[u][5] * inv, f[u][6] * inv, f[u][7] * inv);
           *(u32x2*)(y + (long long)r * ldy + c) = o;
         }
       }
@@ -82,14 +96,15 @@ __global__ __launch_bounds__(256) void quant_fp8_k(const T* __restrict__ x, long
   if (collect) wave_amax_atomic(m, state);
 }
 
-// scale = amax / (448 / 2^margin); a zero amax (all-zero tensor) keeps the previous scale
+// scale = amax / (fmt max / 2^margin); a zero amax (all-zero tensor) keeps the previous scale.
+// state[3] = the format's max finite value (0: e4m3's 448; 57344 for e5m2 gradient states)
 __global__ void fp8_update_k(float* state, int nstates, float margin) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nstates) return;
   float* s = state + 4 * i;
   const float amax = __uint_as_float(*(const unsigned*)&s[2]);
   if (amax > 0.f) {
-    const float sc = amax * margin / FP8_MAX;
+    const float sc = amax * margin / (s[3] > 0.f ? s[3] : FP8_MAX);
     s[0] = sc;
     s[1] = 1.f / sc;
   }
@@ -98,10 +113,10 @@ __global__ void fp8_update_k(float* state, int nstates, float margin) {
 
 // Multi-tensor weight preparation: one launch per pass over every fp8 weight copy.
 struct Fp8Rec {
-  const float* x; long long ldx; int P, C;
-  unsigned char* y; long long ldy;
+  const void* x; long long ldx; int P, C;    // x fp32, or bf16 when xbf16 (e.g. the transposed
+  unsigned char* y; long long ldy;           // bf16 dgrad weight copy)
   float* state;
-  long long pad;
+  long long xbf16;
 };
 static_assert(sizeof(Fp8Rec) == 56, "Fp8Rec layout is shared with cosnet_amd/ops.py");
 
@@ -116,8 +131,12 @@ __global__ __launch_bounds__(256) void quant_fp8_multi_k(const Fp8Rec* __restric
     for (int cc = threadIdx.x; cc < cpr; cc += blockDim.x) {
       const int c = cc * 8;
       float f[8];
-      *(f32x4*)&f[0] = *(const f32x4*)(r.x + row * r.ldx + c);
-      *(f32x4*)&f[4] = *(const f32x4*)(r.x + row * r.ldx + c + 4);
+      if (r.xbf16) {
+        Chunk<bf16>::unpack(*(const u32x4*)((const bf16*)r.x + row * r.ldx + c), f);
+      } else {
+        *(f32x4*)&f[0] = *(const f32x4*)((const float*)r.x + row * r.ldx + c);
+        *(f32x4*)&f[4] = *(const f32x4*)((const float*)r.x + row * r.ldx + c + 4);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
       if (quantise) {
@@ -137,7 +156,7 @@ __global__ void fp8_update_list_k(const Fp8Rec* __restrict__ recs, int n, float 
   float* s = recs[i].state;
   const float amax = __uint_as_float(*(const unsigned*)&s[2]);
   if (amax > 0.f) {
-    const float sc = amax * margin / FP8_MAX;
+    const float sc = amax * margin / (s[3] > 0.f ? s[3] : FP8_MAX);
     s[0] = sc;
     s[1] = 1.f / sc;
   }
@@ -146,9 +165,10 @@ __global__ void fp8_update_list_k(const Fp8Rec* __restrict__ recs, int n, float 
 
 }  // namespace
 
-extern "C" int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int C, void* y8,
-                            long long ldy, float* state, int mode, hipStream_t st) {
+extern "C" int cn_fp8_quant_fmt(int dtype, int fmt, const void* x, long long ldx, int P, int C,
+                                void* y8, long long ldy, float* state, int mode, hipStream_t st) {
   if (C % 8 || ldx % 8 || ldy % 8 || !state) return CN_ERR_ALIGN;
+  if (fmt != 0 && fmt != 1) return CN_ERR_UNSUPPORTED;
   if (P <= 0) return 0;
   const int gx = (C / 8 + 63) / 64;
   int gy = (P + 63) / 64;                      // >= 16 rows per thread
@@ -157,11 +177,17 @@ extern "C" int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int 
   if (gy < 1) gy = 1;
   const dim3 grid(gx, gy);
   auto launch = [&](int quantise, int collect) {
-    if (dtype == DT_BF16)
-      hipLaunchKernelGGL(quant_fp8_k<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ldx, P, C,
+    if (dtype == DT_BF16 && fmt == 0)
+      hipLaunchKernelGGL((quant_fp8_k<bf16, 0>), grid, dim3(256), 0, st, (const bf16*)x, ldx, P, C,
+                         (unsigned char*)y8, ldy, state, quantise, collect);
+    else if (dtype == DT_BF16)
+      hipLaunchKernelGGL((quant_fp8_k<bf16, 1>), grid, dim3(256), 0, st, (const bf16*)x, ldx, P, C,
+                         (unsigned char*)y8, ldy, state, quantise, collect);
+    else if (fmt == 0)
+      hipLaunchKernelGGL((quant_fp8_k<float, 0>), grid, dim3(256), 0, st, (const float*)x, ldx, P, C,
                          (unsigned char*)y8, ldy, state, quantise, collect);
     else
-      hipLaunchKernelGGL(quant_fp8_k<float>, grid, dim3(256), 0, st, (const float*)x, ldx, P, C,
+      hipLaunchKernelGGL((quant_fp8_k<float, 1>), grid, dim3(256), 0, st, (const float*)x, ldx, P, C,
                          (unsigned char*)y8, ldy, state, quantise, collect);
   };
   if (dtype != DT_BF16 && dtype != DT_F32) return CN_ERR_UNSUPPORTED;
@@ -180,6 +206,11 @@ extern "C" int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int 
   }
   CN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int C, void* y8,
+                            long long ldy, float* state, int mode, hipStream_t st) {
+  return cn_fp8_quant_fmt(dtype, 0, x, ldx, P, C, y8, ldy, state, mode, st);
 }
 
 // Current scaling of a list of fp32 tensors (e.g. every fp8 conv-weight copy after the SGD

@@ -477,7 +477,9 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)  // e4m3 x e4m3, unit block scales (E8M0 127 = 2^0)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+          // A format: 0 = e4m3 (forward activations), 1 = e5m2 (gradients, dgrad); B: e4m3 weights
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              af[i], bfr[j], acc[i][j], std::is_same<T, f8e5m2>::value ? 1 : 0, 0, 0, 127, 0, 127);
       return;
     }
 #pragma unroll
@@ -942,13 +944,13 @@ static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_
 
 // fp8 (e4m3) operands: k-contiguous loaders only (conv forward / dgrad / dense products), the
 // three tiles the shape heuristic uses; 128 fp8 per 128-byte K tile, one scaled MFMA per tile.
-template <class CT, int LA>
+template <class CT, int LA, class T8 = f8e4m3>
 static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
   // (the 256x256 tile would spill its fp8 fragments: 128x128 serves the wide products too)
   const int c = pick_cfg(a, batch);
-  if (c == 12) return launch_c<f8e4m3, CT, 12, LA, L_KC_DENSE>(a, batch, st);
-  if (c == 13) return launch_c<f8e4m3, CT, 13, LA, L_KC_DENSE>(a, batch, st);
-  return launch_c<f8e4m3, CT, 11, LA, L_KC_DENSE>(a, batch, st);
+  if (c == 12) return launch_c<T8, CT, 12, LA, L_KC_DENSE>(a, batch, st);
+  if (c == 13) return launch_c<T8, CT, 13, LA, L_KC_DENSE>(a, batch, st);
+  return launch_c<T8, CT, 11, LA, L_KC_DENSE>(a, batch, st);
 }
 
 // 32-bit byte-offset limits of the buffer-descriptor loaders (Loader, BUF path)
@@ -964,7 +966,7 @@ static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
-  const int esz = dtype == DT_FP8 ? 1 : dtype == DT_BF16 ? 2 : 4;
+  const int esz = (dtype == DT_FP8 || dtype == DT_FP8_E5M2) ? 1 : dtype == DT_BF16 ? 2 : 4;
   const int bk = 128 / esz;
   // conv gathers whose K tiles can straddle taps, or too large for 32-bit offsets: per-thread
   // pointer loader
@@ -975,6 +977,13 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     if (la == L_KC_DENSE) return c_f32 ? launch_f8<float, L_KC_DENSE>(a, batch, st) : launch_f8<bf16, L_KC_DENSE>(a, batch, st);
     if (la == L_KC_CONV) return c_f32 ? launch_f8<float, L_KC_CONV>(a, batch, st) : launch_f8<bf16, L_KC_CONV>(a, batch, st);
     if (la == L_KC_CONV_G) return c_f32 ? launch_f8<float, L_KC_CONV_G>(a, batch, st) : launch_f8<bf16, L_KC_CONV_G>(a, batch, st);
+    return CN_ERR_UNSUPPORTED;
+  }
+  if (dtype == DT_FP8_E5M2) {   // dgrad: e5m2 output gradients x e4m3 transposed weights, bf16 dX
+    if (lb != L_KC_DENSE || a.st_mode || a.nsplit != 1 || c_f32) return CN_ERR_UNSUPPORTED;
+    if (la == L_KC_DENSE) return launch_f8<bf16, L_KC_DENSE, f8e5m2>(a, batch, st);
+    if (la == L_KC_CONV) return launch_f8<bf16, L_KC_CONV, f8e5m2>(a, batch, st);
+    if (la == L_KC_CONV_G) return launch_f8<bf16, L_KC_CONV_G, f8e5m2>(a, batch, st);
     return CN_ERR_UNSUPPORTED;
   }
   if (a.st_mode) {

@@ -157,10 +157,33 @@ def stem_bwd(item, dout, grads):
     grads[res.bn1.bias] = db
 
 
-def dgrad_bn_bwd(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn, grads):
+def fp8_dgrad_ok(dy, k):
+    """fp8 dgrad (e5m2 dY x e4m3 W^T) for the compute-heavy stride-1 convs: K = k*k*Cout >= 2304
+    (the layer-3/4 3x3 convs, the ASPP convs); the short-K 1x1 dgrads are HBM-bound and gain
+    nothing from a 2x MFMA rate."""
+    return (dy.dtype == torch.bfloat16 and k * k * dy.shape[1] >= 2304 and dy.shape[1] % 16 == 0
+            and ops.ld(dy) % 16 == 0 and dy.shape[0] > 64)
+
+
+def dgrad(dy, n, oh, ow, wt, cin, k, pad, dil, h, w, weight, ctx, out=None, accumulate=False):
+    """Stride-1 conv dgrad: in fp8 mode (ctx, BASELINE configs[4]) e5m2 output gradients
+    (delayed scaling, ctx.grads) x the e4m3 transposed weight on the block-scaled MFMA."""
+    if ctx is not None and fp8_dgrad_ok(dy, k):
+        dy8, ds = ctx.grads.quant(dy, ("dgrad", id(weight)))
+        wt8, ws = ctx.weights.get_t(weight, wt)
+        return ops.conv_dgrad_fp8(dy8, n, oh, ow, wt8, cin, k, pad, dil, h, w, ds, ws, out=out,
+                                  accumulate=accumulate)
+    return conv_dgrad(dy, n, oh, ow, wt, cin, k, 1, pad, dil, h, w, out=out, accumulate=accumulate)
+
+
+def dgrad_bn_bwd(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn, grads, weight=None, ctx=None):
     """Stride-1 conv dgrad followed by the backward of the BN + ReLU (mask from x) that fed the
     conv: returns (dx of the BN input, dgamma, dbeta)."""
     dgo, dbo = grads.buf(bn.weight, cin), grads.buf(bn.bias, cin)
+    if ctx is not None and fp8_dgrad_ok(dy, k):
+        dyb = dgrad(dy, n, oh, ow, wt, cin, k, pad, dil, oh, ow, weight, ctx)
+        dx, dg, db, _ = bn_bwd(x, dyb, None, stats, bn, act=1, dgamma=dgo, dbeta=dbo)
+        return dx, dg, db
     if fuse_bwd(cin, wt.shape[1]):
         dyb, dg, db = ops.conv_dgrad_bn(dy, n, oh, ow, wt, cin, k, pad, dil, x, stats, bn,
                                         dgamma=dgo, dbeta=dbo)
@@ -222,10 +245,13 @@ def bottleneck_bwd(item, dy, grads, need_dx=True):
                      dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
     # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where
     # that is cheaper (fuse_bwd)
-    dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads)
+    f8 = getattr(blk.bn2, "_cn_fp8", None)
+    dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads,
+                                 weight=blk.conv3.weight, ctx=f8)
     dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
                      dw=grads.buf(blk.conv2.weight, planes, 9 * planes))
-    dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1, grads)
+    dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1, grads,
+                                 weight=blk.conv2.weight, ctx=f8)
     dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1,
                      dw=grads.buf(blk.conv1.weight, planes, cin))
     if need_dx:
@@ -317,7 +343,8 @@ def aspp_bwd(item, dout, grads):
                    dw=grads.buf(mod.bottleneck.weight, 256, 9 * 2560)), mod.bottleneck.weight)
     grads[mod.bottleneck.bias] = ops.colsum(dcb, out=grads.buf(mod.bottleneck.bias, 256))
     grads[mod.bn.weight], grads[mod.bn.bias], grads[pw] = dgb, dbb, dpr
-    dcat = conv_dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, 1, h, w)
+    f8 = getattr(mod.bn, "_cn_fp8", None)
+    dcat = dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, h, w, mod.bottleneck.weight, f8)
     dx = None
     bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
     cms = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
@@ -330,8 +357,8 @@ def aspp_bwd(item, dout, grads):
                        dw=grads.buf(cms[bi].weight, 512, k * k * 2048)), cms[bi].weight)
         grads[cms[bi].bias] = ops.colsum(dci, out=grads.buf(cms[bi].bias, 512))
         grads[bns[bi].weight], grads[bns[bi].bias] = dgi, dbi
-        dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
-                        accumulate=dx is not None)
+        dx = dgrad(dci, n, h, w, wt, 2048, k, dd, max(dd, 1), h, w, cms[bi].weight, f8, out=dx,
+                   accumulate=dx is not None)
     dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
     ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
     dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp[0], mod.bn_x, act=1,
@@ -370,6 +397,7 @@ class EncoderPairFn(F):
         half = out.shape[0] // 2
         ctx.rec = rec
         ctx.params = params
+        ctx.enc = enc
         ctx.training = enc.training
         ctx.defer = getattr(enc, "_cn_defer", None) if rec is not None else None
         ctx.set_materialize_grads(False)
@@ -392,10 +420,15 @@ class EncoderPairFn(F):
             ctx.defer.stash(rec, dfa)
             return (None,) * (3 + len(ctx.params))
         grads = GradSink()
+        f8 = getattr(ctx.enc, "_cn_fp8", None)
+        if f8 is not None:
+            f8.grads.begin()
         dx = aspp_bwd(rec[-1], dfa, grads)
         for item in reversed(rec[1:-1]):
             dx = bottleneck_bwd(item, dx, grads)
         stem_bwd(rec[0], dx, grads)
+        if f8 is not None:
+            f8.grads.end()   # advance the gradient scales from this backward's amax
         return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
 
 
@@ -441,6 +474,9 @@ class DeferredEncoderBwd:
     def run(self, k):
         rec, grads = self.rec, GradSink(self.arena)
         by_blk = {it[1]: it for it in rec[1:-1]}
+        f8 = getattr(self.enc, "_cn_fp8", None)
+        if f8 is not None and k == 0:
+            f8.grads.begin()
         for it in self.plan[k]:
             if it == "aspp":
                 self.dx = aspp_bwd(rec[-1], self.dfa, grads)
@@ -450,6 +486,8 @@ class DeferredEncoderBwd:
                 self.dx = bottleneck_bwd(by_blk[it], self.dx, grads)
         if k == len(self.plan) - 1:
             self.rec = self.dfa = self.dx = None
+            if f8 is not None:
+                f8.grads.end()
         return grads
 
 

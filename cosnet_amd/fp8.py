@@ -13,6 +13,12 @@ bf16 path.
   convs that read it) with the scale derived from the previous step's amax of that tensor,
   while this step's amax is collected; one cn_fp8_update per encoder pass advances all scales.
   A state is calibrated (amax pass) on first use, so step 0 does not saturate.
+* Gradients (dgrad): the output gradient of a compute-heavy stride-1 conv (K = kh*kw*Cout >=
+  2304: the 3x3 layer-3/4 convs, the ASPP convs) is quantised to e5m2 (range over precision,
+  the usual gradient format) with delayed scaling of its own (Fp8Context.grads, updated once
+  per encoder backward), and multiplied with an e4m3 copy of the transposed weight (current
+  scaling, refreshed with the forward copies after every SGD step) -- cn_conv_dgrad_fp8, the
+  block-scaled MFMA with A format e5m2.  Weight gradients stay bf16 x bf16.
 """
 import struct
 import weakref
@@ -23,7 +29,7 @@ import torch
 from . import _native as nv
 from . import ops
 
-_REC = struct.Struct("<QqiiQqQq")   # Fp8Rec (fp8.hip): x, ldx, P, C, y, ldy, state, pad
+_REC = struct.Struct("<QqiiQqQq")   # Fp8Rec (fp8.hip): x, ldx, P, C, y, ldy, state, x_is_bf16
 assert _REC.size == 56
 
 
@@ -35,7 +41,8 @@ class Fp8Weights:
     """fp8 copies of fp32 conv weights (channels_last), refreshed after each optimiser step."""
 
     def __init__(self):
-        self._c = {}          # id(w) -> [wf8, state, tag, w]
+        self._c = {}          # id(w) -> [wf8, state, tag, w, src]; ("t", id(w)) -> the transposed
+                              # dgrad copy (src = the bf16 [Cin][KH*KW*Cout] weight-cache copy)
         self._table = None
         self._table_n = 0
         self._table_ptrs = None   # the master / copy addresses the table was packed with
@@ -55,7 +62,7 @@ class Fp8Weights:
             cout = w.shape[0]
             k = w.numel() // cout
             wf8 = torch.empty((cout, k), dtype=torch.uint8, device=w.device)
-            e = [wf8, ops.fp8_state(w.device), None, w]
+            e = [wf8, ops.fp8_state(w.device), None, w, None]
             self._c[id(w)] = e
             self._table = None
         if e[2] != self._tag(w):
@@ -67,8 +74,29 @@ class Fp8Weights:
             e[2] = self._tag(w)
         return e[0], e[1]
 
+    def get_t(self, w, wt):
+        """e4m3 copy of the transposed weight wt (bf16 [Cin][KH*KW*Cout], the dgrad operand of
+        the weight cache), refreshed from wt with current scaling; (wt8, state)."""
+        key = ("t", id(w))
+        e = self._c.get(key)
+        if e is None:
+            if self._captured:
+                raise RuntimeError("new fp8 weight after a graph captured this context's "
+                                   "refresh table (re-capture the step)")
+            e = [torch.empty(tuple(wt.shape), dtype=torch.uint8, device=wt.device),
+                 ops.fp8_state(wt.device), None, w, wt]
+            self._c[key] = e
+            self._table = None
+        if e[2] != self._tag(w):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fp8 weight copy is stale inside a graph capture")
+            ops.fp8_quant(wt, e[1], ops.FP8_CURRENT, out=e[0])
+            e[2] = self._tag(w)
+        return e[0], e[1]
+
     def _ptrs(self):
-        return tuple((e[3].data_ptr(), e[0].data_ptr(), e[1].data_ptr()) for e in self._c.values())
+        return tuple((e[3].data_ptr(), e[0].data_ptr(), e[1].data_ptr(),
+                      e[4].data_ptr() if e[4] is not None else 0) for e in self._c.values())
 
     def refresh_all(self):
         """Re-quantise every fp8 copy from its (just updated) master: 3 launches."""
@@ -87,10 +115,15 @@ class Fp8Weights:
             if capturing:
                 raise RuntimeError("fp8 weight table must be built before graph capture")
             blob = b""
-            for wf8, st, _, w in self._c.values():
-                cin = w.shape[1]
-                blob += _REC.pack(w.data_ptr(), cin, w.numel() // cin, cin, wf8.data_ptr(), cin,
-                                  st.data_ptr(), 0)
+            for wf8, st, _, w, src in self._c.values():
+                if src is None:   # forward copy from the fp32 master [Cout][KH][KW][Cin]
+                    cin = w.shape[1]
+                    blob += _REC.pack(w.data_ptr(), cin, w.numel() // cin, cin, wf8.data_ptr(), cin,
+                                      st.data_ptr(), 0)
+                else:             # transposed dgrad copy from the bf16 weight-cache copy
+                    p_, c_ = src.shape
+                    blob += _REC.pack(src.data_ptr(), ops.ld(src), p_, c_, wf8.data_ptr(), c_,
+                                      st.data_ptr(), 1)
             host = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy())
             dev = next(iter(self._c.values()))[0].device
             self._table = host.to(dev)
@@ -110,10 +143,12 @@ class Fp8Weights:
 
 
 class Fp8Acts:
-    """Delayed-scaling states of the conv inputs, in one device buffer (one update launch)."""
+    """Delayed-scaling states of the conv inputs (e4m3) or of the dgrad output gradients
+    (fmt=e5m2), in one device buffer (one update launch)."""
 
-    def __init__(self, cap=1024):
+    def __init__(self, cap=1024, fmt=ops.FP8_E4M3):
         self.cap = cap
+        self.fmt = fmt
         self.states = None
         self.slots = {}
         self.calibrated = set()
@@ -124,8 +159,8 @@ class Fp8Acts:
 
     def state(self, key, device):
         if self.states is None:
-            self.states = torch.tensor([[1.0, 1.0, 0.0, 0.0]] * self.cap, dtype=torch.float32,
-                                       device=device)
+            self.states = torch.tensor([[1.0, 1.0, 0.0, ops.FMT_MAX[self.fmt]]] * self.cap,
+                                       dtype=torch.float32, device=device)
         i = self.slots.get(key)
         if i is None:
             i = len(self.slots)
@@ -144,10 +179,10 @@ class Fp8Acts:
         if i not in self.calibrated:   # first use: this tensor's own amax sets the scale
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("fp8 activation state first used inside a graph capture")
-            ops.fp8_quant(x, st, ops.FP8_AMAX)
+            ops.fp8_quant(x, st, ops.FP8_AMAX, fmt=self.fmt)
             ops.fp8_update(st)
             self.calibrated.add(i)
-        x8 = ops.fp8_quant(x, st, ops.FP8_DELAYED)
+        x8 = ops.fp8_quant(x, st, ops.FP8_DELAYED, fmt=self.fmt)
         self.pass_cache[ck] = (x8, st, x)   # x held: its address cannot be reused this pass
         return x8, st
 
@@ -176,6 +211,7 @@ class Fp8Context:
     def __init__(self):
         self.weights = Fp8Weights()
         self.acts = Fp8Acts()
+        self.grads = Fp8Acts(fmt=ops.FP8_E5M2)
         LIVE.add(self)
 
 

@@ -249,20 +249,25 @@ def bn_bwd_apply(x, dy, stats, bn, dgamma, dbeta, out=None):
 
 
 # ---- fp8 (e4m3) operands (BASELINE configs[4]) ------------------------------------------------
-def fp8_state(device):
-    """Per-tensor fp8 scaling state [scale, 1/scale, amax, -] (cn_fp8_quant)."""
-    return torch.tensor([1.0, 1.0, 0.0, 0.0], dtype=torch.float32, device=device)
+FP8_E4M3, FP8_E5M2 = 0, 1
+FMT_MAX = {FP8_E4M3: 448.0, FP8_E5M2: 57344.0}
+
+
+def fp8_state(device, fmt=FP8_E4M3):
+    """Per-tensor fp8 scaling state [scale, 1/scale, amax, format max] (cn_fp8_quant_fmt)."""
+    return torch.tensor([1.0, 1.0, 0.0, FMT_MAX[fmt]], dtype=torch.float32, device=device)
 
 
 FP8_DELAYED, FP8_CURRENT, FP8_AMAX = 0, 1, 2
 
 
-def fp8_quant(x, state, mode=FP8_CURRENT, out=None):
-    """x [P, C] (fp32 / bf16) -> e4m3 bytes [P, C] (uint8) scaled by state (see fp8_state)."""
+def fp8_quant(x, state, mode=FP8_CURRENT, out=None, fmt=FP8_E4M3):
+    """x [P, C] (fp32 / bf16) -> fp8 bytes [P, C] (uint8; e4m3, or e5m2 with fmt=FP8_E5M2)
+    scaled by state (see fp8_state)."""
     p, c = x.shape
     if out is None and mode != FP8_AMAX:
         out = torch.empty((p, c), dtype=torch.uint8, device=x.device)
-    nv.call("cn_fp8_quant", dtc(x), x.data_ptr(), ld(x), p, c, nv.ptr(out),
+    nv.call("cn_fp8_quant_fmt", dtc(x), fmt, x.data_ptr(), ld(x), p, c, nv.ptr(out),
             ld(out) if out is not None else c, state.data_ptr(), mode, nv.stream())
     return out
 
@@ -270,6 +275,21 @@ def fp8_quant(x, state, mode=FP8_CURRENT, out=None):
 def fp8_update(states, margin=1.0):
     """Turn each state's collected amax into its next scale (states: [n, 4] or [4])."""
     nv.call("cn_fp8_update", states.data_ptr(), states.numel() // 4, float(margin), nv.stream())
+
+
+def conv_dgrad_fp8(dy8, n, oh, ow, wt8, cin, k, pad, dil, h, w, dy_state, w_state, out=None,
+                   accumulate=False):
+    """dx (bf16) (+)= conv_dgrad(dy8 e5m2, wt8 e4m3) * s_dy * s_w, stride 1 (fp8 mode)."""
+    cout = wt8.shape[1] // (k * k)
+    if out is None:
+        out = torch.empty((n * h * w, cin), dtype=torch.bfloat16, device=dy8.device)
+    ev = _prof_start(2.0 * n * h * w * cin * k * k * cout, ("dgrad8", n * h * w, cin, k * k * cout),
+                     n * oh * ow * cout + cin * k * k * cout + 2 * n * h * w * cin)
+    nv.call("cn_conv_dgrad_fp8", dy8.data_ptr(), ld(dy8), n, oh, ow, cout, wt8.data_ptr(), cin, k, k,
+            pad, dil, out.data_ptr(), ld(out), h, w, int(accumulate), dy_state.data_ptr(),
+            w_state.data_ptr(), nv.stream())
+    _prof_end(ev)
+    return out
 
 
 def conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, bias=None,

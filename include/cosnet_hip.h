@@ -63,12 +63,27 @@ int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, f
  * x: [P][C] (ldx) fp32 or bf16, C % 8 == 0; y8: [P][C] bytes (ldy). */
 int cn_fp8_quant(int dtype, const void* x, long long ldx, int P, int C, void* y8, long long ldy,
                  float* state, int mode, hipStream_t stream);
-/* Current scaling of n fp32 matrices in three launches (amax, update, quantise): device table
- * of n records {const float* x; long long ldx; int P, C; uint8* y; long long ldy; float* state;
- * long long pad} (56 bytes each) -- the fp8 copies of the conv weights after each SGD step. */
+/* The same with the output format chosen: fmt 0 = e4m3 (max 448), 1 = e5m2 (max 57344; the
+ * output gradients of the fp8 dgrad).  An e5m2 state carries state[3] = 57344 (the update's
+ * format max; 0 means e4m3). */
+int cn_fp8_quant_fmt(int dtype, int fmt, const void* x, long long ldx, int P, int C, void* y8,
+                     long long ldy, float* state, int mode, hipStream_t stream);
+/* Current scaling of n matrices in three launches (amax, update, quantise): device table of n
+ * records {const void* x; long long ldx; int P, C; uint8* y; long long ldy; float* state;
+ * long long x_is_bf16} (56 bytes each) -- the fp8 copies of the conv weights (fp32 masters) and
+ * of the transposed dgrad weights (bf16 copies) after each SGD step. */
 int cn_fp8_quant_multi(const void* recs, int n, hipStream_t stream);
-/* scale = amax * margin / 448 for each of nstates consecutive states; amax reset */
+/* scale = amax * margin / fmt max (state[3], default 448) for each of nstates consecutive
+ * states; amax reset */
 int cn_fp8_update(float* states, int nstates, float margin, hipStream_t stream);
+/* dx (bf16) (+)= conv_dgrad(dy8, wt8) * dy_state[0] * w_state[0], stride 1 (replaces the
+ * backward of nn.Conv2d w.r.t. its input, deeplab/residual_net.py:59-67 autograd, in fp8 mode):
+ * dy8 e5m2 [N*OH*OW][Cout] (cn_fp8_quant_fmt fmt 1), wt8 e4m3 [Cin][KH][KW][Cout]; block-scaled
+ * MFMA with A format e5m2, B e4m3.  Cout % 16 == 0; accumulate: dx += (else dx =). */
+int cn_conv_dgrad_fp8(const void* dy8, long long lddy, int N, int OH, int OW, int Cout,
+                      const void* wt8, int Cin, int KH, int KW, int pad, int dil, void* dx,
+                      long long lddx, int H, int W, int accumulate, const float* dy_state,
+                      const float* w_state, hipStream_t stream);
 /* y (bf16) = conv2d(x8, w8) * x_state[0] * w_state[0] + bias: the fp8 implicit-GEMM conv
  * (block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales).  Cin % 16 == 0. */
 int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin, const void* w8,

@@ -665,6 +665,59 @@ def test_conv_fwd_fp8(cuda, case):
     assert err <= 1e-2, err
 
 
+def _dec_e5m2(y8):
+    return y8.cpu().view(torch.float8_e5m2).double()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fp8_quant_e5m2_matches_torch(cuda, dt):
+    """cn_fp8_quant_fmt fmt 1 (the dgrad output gradients): scale = amax / 57344, bytes =
+    e5m2(x / scale) saturating, against torch's float8_e5m2 conversion (round to nearest even)."""
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn((300, 96), generator=g) * 1e-3).to(dt)
+    st = ops.fp8_state(cuda, ops.FP8_E5M2)
+    y8 = ops.fp8_quant(x.to(cuda), st, ops.FP8_CURRENT, fmt=ops.FP8_E5M2)
+    torch.cuda.synchronize()
+    amax = x.double().abs().max().item()
+    assert abs(st[0].item() - amax / 57344) <= 1e-6 * amax
+    ref = (x.double() * st[1].double().cpu()).clamp(-57344, 57344).to(torch.float8_e5m2)
+    got = _dec_e5m2(y8)
+    diff = (got - ref.double()).abs()
+    ulp = ref.double().abs().clamp_min(2 ** -14) * 2 ** -2   # one e5m2 mantissa step
+    assert (diff <= ulp * 1.001).all()
+    assert (diff == 0).double().mean().item() >= 0.999
+
+
+@pytest.mark.parametrize("case", [(2, 256, 13, 11, 128, 3, 1, 1), (2, 128, 15, 9, 64, 1, 0, 1),
+                                  (4, 512, 30, 30, 512, 3, 4, 4), (2, 256, 60, 60, 256, 3, 2, 2)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad_fp8(cuda, case, accumulate):
+    """cn_conv_dgrad_fp8 (stride 1) against fp64 conv_transpose of the exactly-decoded e5m2 dY and
+    e4m3 W^T times their scales: the A-format-e5m2 MFMA's operand map and the dequantisation; only
+    fp32 accumulation and the bf16 output rounding remain (1e-2 of the output scale)."""
+    n, cout, h, w, cin, k, p, d = case
+    dy = rnd((n, cout, h, w), torch.float32, 41, scale=1e-2)
+    wt = rnd((cout, cin, k, k), torch.float32, 42, scale=(2.0 / (cin * k * k)) ** 0.5)
+    ds, ws = ops.fp8_state(cuda, ops.FP8_E5M2), ops.fp8_state(cuda)
+    dy8 = ops.fp8_quant(nhwc(dy).float().to(cuda).contiguous(), ds, ops.FP8_CURRENT, fmt=ops.FP8_E5M2)
+    # transposed weight [Cin][KH][KW][Cout] (the weight cache's dgrad copy)
+    wT = wt.permute(1, 2, 3, 0).reshape(cin, k * k * cout).float().to(cuda).contiguous()
+    w8 = ops.fp8_quant(wT, ws, ops.FP8_CURRENT)
+    base = rnd((n, cin, h, w), torch.float32, 43)
+    dx = nhwc(base).to(torch.bfloat16).to(cuda).contiguous()
+    dx0 = dx.double().cpu()
+    ops.conv_dgrad_fp8(dy8, n, h, w, w8, cin, k, p, d, h, w, ds, ws, out=dx, accumulate=accumulate)
+    torch.cuda.synchronize()
+    dyq = nchw(_dec_e5m2(dy8), n, h, w) * ds[0].double().cpu()
+    wq = _dec_e4m3(w8).reshape(cin, k, k, cout).permute(3, 0, 1, 2) * ws[0].double().cpu()
+    ref = F.conv_transpose2d(dyq, wq, None, 1, p, 0, 1, d)
+    if accumulate:
+        ref = ref + nchw(dx0, n, h, w)
+    got = nchw(dx, n, h, w).double().cpu()
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 1e-2, err
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("c", [3, 1])
 def test_nchw_to_nhwc(cuda, dt, c):
