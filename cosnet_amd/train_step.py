@@ -121,6 +121,13 @@ class TrainStep:
         self.opt.step()
 
     # ---- data parallel: arena, buckets, deferred encoder backward ----------------------------
+    def _bind(self):
+        """Point the encoders' deferred-backward holders at THIS step's (several TrainSteps may
+        share one model: ShapeGraphCache keeps one per frame size)."""
+        if self.dp is not None:
+            for e, d in zip((self.model.encoder, self.model.depth_encoder), self.dp["defers"]):
+                e._cn_defer = d
+
     def _dp_setup(self):
         from .encoder_fn import DeferredEncoderBwd
         m = self.model
@@ -166,7 +173,7 @@ class TrainStep:
             half = torch.zeros((n,), dtype=torch.bfloat16, device=dev)
         self.dp = {"buckets": buckets, "ranges": ranges, "segs": segs, "flat": flat, "arena": arena,
                    "views": views, "head": head, "half": half, "works": [], "graphs": None,
-                   "head_live": None}
+                   "head_live": None, "defers": defers}
         self.flat = flat
 
     def _dp_forward_backward(self):
@@ -268,6 +275,7 @@ class TrainStep:
         """Run `warmup` eager iterations (they are real steps) on a side stream, then record."""
         if self.world > 1 and self.dp is None:
             self._dp_setup()
+        self._bind()
         if not self.graphed:
             for _ in range(warmup):
                 self._eager_once()
@@ -279,6 +287,7 @@ class TrainStep:
         s = self.stream
         for _ in range(warmup):
             self._eager_once()
+        warm_loss = self.loss.clone() if warmup else None   # the last real step's loss
         torch.cuda.synchronize()
         self.opt.reserve()
         self.opt.freeze_for_capture()
@@ -296,6 +305,8 @@ class TrainStep:
         finally:
             self._capturing = False
         self._graph_loss = self.loss
+        if warm_loss is not None:
+            self.loss = warm_loss   # recording computed nothing: report the warm-up step's loss
         after = self._bn_counts()
         self._nbt_delta = {m: after[m] - before[m] for m in after if after[m] != before[m]}
         for m, k in before.items():  # recording executed nothing: only replays count
@@ -364,6 +375,7 @@ class TrainStep:
     def _eager_once(self):
         if self.world > 1 and self.dp is None:
             self._dp_setup()
+        self._bind()
 
         def once():
             self._counts()
@@ -400,3 +412,56 @@ class TrainStep:
         if self.world > 1:
             for b in self.model.buffers():
                 dist.broadcast(b, src, group=self.group)
+
+
+class ShapeGraphCache:
+    """Recorded steps keyed by frame size, for inputs whose size changes from batch to batch (the
+    SBM-RGBD loader's per-batch random scale x crop, dataloaders/sbm_rgbd_loader.py:700-702,
+    :710-722): a size seen `min_hits` times gets its own TrainStep, recorded on that batch (the
+    recording run is a real eager step) and replayed on every later batch of that size; other
+    sizes run eagerly (TrainStep.run_batch).  Up to `capacity` sizes are kept (least recently used
+    evicted: its graph and memory pool are released).  All steps share the model, the optimiser
+    and its state, so the trajectory is the same whichever path a batch takes (graph replay and
+    eager step run the same kernels in the same order: bitwise equal)."""
+
+    def __init__(self, model, opt, batch, l1_weight=0.8, grad_dtype="fp32", capacity=24, min_hits=2):
+        from collections import OrderedDict
+        self.model, self.opt, self.batch = model, opt, batch
+        self.l1, self.grad_dtype = l1_weight, grad_dtype
+        self.capacity, self.min_hits = capacity, min_hits
+        self.graphs = OrderedDict()      # (h, w) -> TrainStep (recorded)
+        self.seen = {}
+        self.eager = None
+        self.hits = self.records = self.eager_steps = 0
+
+    def __call__(self, rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b, lrs):
+        hw = tuple(rgb_a.shape[2:])
+        ins = (rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b)
+        st = self.graphs.get(hw)
+        if st is not None:
+            self.graphs.move_to_end(hw)
+            self.hits += 1
+            st.load(*ins)
+            return st(lrs)
+        self.seen[hw] = self.seen.get(hw, 0) + 1
+        if self.seen[hw] >= self.min_hits and self.capacity > 0 and rgb_a.shape[0] == self.batch:
+            if len(self.graphs) >= self.capacity:
+                self.graphs.popitem(last=False)
+            st = TrainStep(self.model, self.opt, self.batch, hw, l1_weight=self.l1, graphed=True,
+                           grad_dtype=self.grad_dtype)
+            st.load(*ins)
+            self.opt.set_lrs(lrs)
+            st.capture(warmup=1)          # this batch's step runs eagerly, then the record
+            self.graphs[hw] = st
+            self.records += 1
+            return st.loss
+        if self.eager is None:
+            self.eager = TrainStep(self.model, self.opt, self.batch, hw, l1_weight=self.l1,
+                                   graphed=False, grad_dtype=self.grad_dtype)
+        self.eager_steps += 1
+        return self.eager.run_batch(*ins, lrs)
+
+    def sync_buffers(self, src=0):
+        st = self.eager or next(iter(self.graphs.values()), None)
+        if st is not None:
+            st.sync_buffers(src)

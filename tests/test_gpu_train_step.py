@@ -108,3 +108,37 @@ def test_two_stream_encoders_match_one_stream(cuda):
     p0 = [p.detach() for p in runs[0][0].parameters()]
     p1 = [p.detach() for p in runs[1][0].parameters()]
     assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+def test_shape_graph_cache_matches_eager(cuda):
+    """ShapeGraphCache (train.py --dataset sbmrgbd: the frame size changes every batch): sizes
+    seen twice are recorded and replayed, others run eagerly; the loss trajectory and the final
+    parameters equal a plain eager run of the same batches (same kernels, same order: bitwise)."""
+    import cosnet_amd as C
+    from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+    from cosnet_amd.optim import SGD, reference_param_groups
+    from cosnet_amd.train_step import ShapeGraphCache, TrainStep
+
+    def model():
+        m = C.build_model(torch.bfloat16)
+        m.load_state_dict(recipe_state_dict(m.state_dict()))
+        m.encoder.main_classifier.requires_grad_(False)
+        m = m.to(cuda).train()
+        g0, g1 = reference_param_groups(m)
+        return m, SGD([g0, g1], [0.0, 0.0], momentum=0.9, weight_decay=5e-4)
+
+    sizes = [(65, 81), (73, 57), (65, 81), (73, 57), (65, 81), (49, 65), (73, 57)]
+    batches = [[t.to(cuda) for t in synthetic_inputs(2, h, w, seed=50 + i)] for i, (h, w) in enumerate(sizes)]
+    lrs = [2.5e-6, 2.5e-3]
+    m1, o1 = model()
+    cache = ShapeGraphCache(m1, o1, 2, capacity=4, min_hits=2)
+    l1 = [float(cache(*b, lrs).item()) for b in batches]
+    m2, o2 = model()
+    eager = TrainStep(m2, o2, 2, sizes[0], graphed=False)
+    l2 = [float(eager.run_batch(*b, lrs).item()) for b in batches]
+    torch.cuda.synchronize()
+    assert cache.records == 2 and cache.hits == 2 and cache.eager_steps == 3, (
+        cache.records, cache.hits, cache.eager_steps)
+    assert l1 == l2, (l1, l2)
+    for (k, a), (_, b) in zip(m1.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k

@@ -68,6 +68,10 @@ def get_arguments(argv=None):
                    help="data-parallel gradient reduction dtype (bucketed, overlapped)")
     p.add_argument("--log-mem", type=int, default=1,
                    help="logMem lines around each iteration like train.py:560-621 (0: off)")
+    p.add_argument("--graph-cache", type=int, default=24,
+                   help="sbmrgbd: recorded steps kept per frame size (0: every batch eager)")
+    p.add_argument("--graph-cache-min-hits", type=int, default=2,
+                   help="sbmrgbd: record a frame size on its n-th occurrence")
     p.add_argument("--gc-every-iter", type=int, default=0,
                    help="1: gc.collect() + torch.cuda.empty_cache() after every iteration as the "
                         "reference does (train.py:619-620); off by default: it costs host time "
@@ -282,6 +286,13 @@ def main(argv=None):
     max_iter = args.maxEpoches * train_len
     step = TrainStep(model, opt, per_rank, args.output_HW, graphed=bool(args.graph) and not sbm,
                      grad_dtype=args.grad_dtype)
+    cache = None
+    if sbm and args.graph and args.graph_cache > 0:
+        # the augmented frames change size every batch (sbm_rgbd_loader.py:700-702): one recorded
+        # step per recurring size instead of ~2000 host launches per batch
+        from cosnet_amd.train_step import ShapeGraphCache
+        cache = ShapeGraphCache(model, opt, per_rank, grad_dtype=args.grad_dtype,
+                                capacity=args.graph_cache, min_hits=args.graph_cache_min_hits)
     mem = (lambda prefix: log_mem(logger, prefix)) if (args.log_mem and is0) else (lambda prefix: None)
     step.mem_hook = mem
     say("=====> Begin to train: %d iterations per epoch, %d epochs, %d GPU(s) x %d pairs" % (
@@ -303,7 +314,9 @@ def main(argv=None):
                    batch["search_0_depth"].to(dev), batch["target_gt"].unsqueeze(1).to(dev).float(),
                    batch["search_0_gt"].unsqueeze(1).to(dev).float())
             mem(" After feeding data to GPU")
-            if sbm:
+            if sbm and cache is not None:
+                loss = cache(*ins, lrs)
+            elif sbm:
                 loss = step.run_batch(*ins, lrs)
             elif not captured:
                 step.load(*ins)
@@ -333,7 +346,7 @@ def main(argv=None):
                 gc.collect()
                 torch.cuda.empty_cache()
             mem(" After GC")
-        step.sync_buffers()  # rank 0's BN buffers, like DataParallel's replica 0
+        (cache if cache is not None else step).sync_buffers()  # rank 0's BN buffers (DataParallel replica 0)
         if is0:
             path = os.path.join(args.snapshot_dir, "snapshot_%s_%d.pth" % (args.dataset, epoch))
             save_snapshot(path, epoch + 1, model, dataparallel_keys=world > 1)
