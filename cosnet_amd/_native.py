@@ -59,6 +59,8 @@ _SIGS = {
     "cn_coatt_fused_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P]),
     "cn_coatt_fused_fwd_ws": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _S, _P]),
     "cn_coatt_fused_workspace_bytes": (_S, [_I, _I, _I]),
+    "cn_coatt_f8_workspace_bytes": (_S, [_I, _I]),
+    "cn_coatt_f8_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
     "cn_coatt_flash_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P]),
     "cn_coatt_flash_pv": (_I, [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _P, _L, _I, _P]),
     "cn_coatt_flash_dvat": (_I, [_P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _I, _I, _I, _P,
@@ -125,7 +127,7 @@ def load():
 
 
 HASHED_SOURCES = ["gemm.hip", "conv.hip", "bn.hip", "ew.hip", "coatt.hip", "coatt_fused.hip",
-                  "coatt_flash.hip", "fp8.hip", "frames.hip", "eval.hip", "common.h", "gemm.h",
+                  "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip", "common.h", "gemm.h",
                   "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
 
 

@@ -1,0 +1,421 @@
+// fp8 (OCP e4m3, MX block-scaled) flash co-attention forward -- BASELINE configs[4]
+// ("fp8 MFMA affinity"): the affinity S = Va_t . Vb^T and the attention gathers P . V of both
+// directions (rgbd_segmentation_RAA.py:160-170 for RGB, :213-221 for depth) on the block-scaled
+// MFMA v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 rate), softmax statistics in fp32.
+//
+// Same flash structure as coatt_fused.hip (one workgroup = 4 waves = 128 query rows, S^T = K Q^T
+// so the online softmax is lane-local, P as the B operand of O^T += V^T P^T), with:
+//   * operands in MX format: e4m3 bytes + one E8M0 exponent per 32 consecutive reduction values
+//     (Q, K: per row and 32-channel block; V: per channel and 32 consecutive keys), applied by
+//     the MFMA itself (scale_a / scale_b) -- a per-block dynamic range instead of one per-tensor
+//     scale.  Operand layout of the scaled 32x32x64 e4m3 MFMA (measured, tools/probes/
+//     mfma_scale_layout.hip): bytes 0-15 of BOTH lane halves form k-block 0 and bytes 16-31
+//     k-block 1; block b is scaled by the scale operand of lane half b.  So lane half h carries
+//     channels [64kk + 16h, +16) and [64kk + 32 + 16h, +16) of MFMA step kk, and a V^T lane the
+//     keys of both 32-key halves of the tile;
+//   * 64-key tiles (one scaled MFMA covers 64 keys of the PV product);
+//   * P (<= 2^8 under the lazy rescale) quantised to e4m3 with unit scale; the row sum l is
+//     accumulated from the fp32 P.
+// A prepass (coatt_f8_rows_k, coatt_f8_vt_k) writes the MX images into a caller-owned workspace:
+//   rows:  X8 [B][HWp][256] bytes, Xs [B][HWp][8] (byte 4h + kk = block 2kk + h, the byte the
+//          lane half h of MFMA step kk needs at opsel kk);
+//   V^T:   VT8 [B][nt][256][64] per 64-key tile, the keys of lane half h in the accumulator order
+//          key(h, j) = 32 (j >> 4) + (j & 3) + 8 ((j & 15) >> 2) + 4 h (so P needs no permute);
+//          VTs [B][nt][2][32][8] (key block u = keys 32u..32u+31 of the tile, row r of a
+//          32-channel block, block dt): lane half h reads block u = h.
+// Padded rows / keys (>= HW) are zeros, so the loads need no bounds checks.
+#include "common.h"
+#include "../../include/cosnet_hip.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int D = 256;            // feature channels
+constexpr int QB = 128;           // query rows per workgroup
+constexpr int KT = 64;            // keys per tile
+constexpr int QBYTES = QB * D;    // 32 KB Q image
+constexpr int KBYTES = KT * D;    // 16 KB K tile image
+constexpr int VBYTES = D * KT;    // 16 KB V^T tile image
+constexpr int SBYTES = 1024;      // K scales (512) + V^T scales (512)
+constexpr int STAGE = KBYTES + VBYTES + SBYTES;
+constexpr int NSTAGE = 3;
+constexpr int NDMA = KBYTES / 4096 + VBYTES / 4096 + 1;   // LDS-DMA instructions per thread per tile
+constexpr float F8MAX = 448.f;
+constexpr float RESC_T = 8.0f;    // lazy rescale threshold (log2): P <= 2^8 fits e4m3 unscaled
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// E8M0 exponent for a block with max |x| = amax: smallest e with amax / 2^(e-127) <= 448
+__device__ __forceinline__ int e8m0_of(float amax) {
+  if (!(amax > 0.f)) return 127;
+  int ex;
+  const float m = frexpf(amax / F8MAX, &ex);   // amax/448 = m 2^ex, m in [0.5, 1)
+  int e = (m == 0.5f) ? ex - 1 : ex;           // ceil(log2(amax / 448))
+  e += 127;
+  return e < 1 ? 1 : (e > 254 ? 254 : e);
+}
+
+__device__ __forceinline__ unsigned pk4(float a, float b, float c, float d) {
+  unsigned w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+
+__device__ __forceinline__ float clampf8(float x) { return fminf(fmaxf(x, -F8MAX), F8MAX); }
+
+// ---- prepass: rows (Q / K images) ------------------------------------------------------------
+// thread = (row, 32-channel block); rows >= HW of each batch entry are zero
+__global__ __launch_bounds__(256) void coatt_f8_rows_k(const bf16* __restrict__ x, long long ldx,
+                                                       int B, int HW, int HWp,
+                                                       unsigned char* __restrict__ x8,
+                                                       unsigned char* __restrict__ xs) {
+  const long long t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= (long long)B * HWp * 8) return;
+  const int bi = (int)(t & 7);
+  const long long prow = t >> 3;
+  const int b = (int)(prow / HWp), r = (int)(prow % HWp);
+  float v[32];
+  if (r < HW) {
+    const bf16* src = x + ((long long)b * HW + r) * ldx + 32 * bi;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Chunk<bf16>::unpack(*(const u32x4*)(src + 8 * q), v + 8 * q);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = 0.f;
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  const int e = e8m0_of(amax);
+  const float inv = ldexpf(1.f, 127 - e);
+  u32x4 o0, o1;
+  unsigned w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    w[i] = pk4(clampf8(v[4 * i] * inv), clampf8(v[4 * i + 1] * inv), clampf8(v[4 * i + 2] * inv),
+               clampf8(v[4 * i + 3] * inv));
+  o0 = {w[0], w[1], w[2], w[3]};
+  o1 = {w[4], w[5], w[6], w[7]};
+  unsigned char* dst = x8 + prow * D + 32 * bi;
+  *(u32x4*)dst = o0;
+  *(u32x4*)(dst + 16) = o1;
+  xs[prow * 8 + 4 * (bi & 1) + (bi >> 1)] = (unsigned char)e;
+}
+
+// ---- prepass: V^T tiles ------------------------------------------------------------------------
+// thread = (b, tile, key block u, channel d): keys 32u .. 32u+31 of the tile at channel d, one
+// E8M0 exponent; key kk of the block goes to lane half h = (kk >> 2) & 1, byte 16u + i with
+// i = (kk & 3) + 4 (kk >> 3), i.e. key(h, j) above
+__global__ __launch_bounds__(256) void coatt_f8_vt_k(const bf16* __restrict__ v, long long ldv, int B,
+                                                     int HW, int nt, unsigned char* __restrict__ vt8,
+                                                     unsigned char* __restrict__ vts) {
+  const long long t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= (long long)B * nt * 2 * D) return;
+  const int d = (int)(t % D);
+  const long long q = t / D;
+  const int u = (int)(q & 1);
+  const long long bt = q >> 1;
+  const int tile = (int)(bt % nt), b = (int)(bt / nt);
+  float x[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    const int key = tile * KT + 32 * u + kk;
+    x[kk] = key < HW ? (float)v[((long long)b * HW + key) * ldv + d] : 0.f;
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) amax = fmaxf(amax, fabsf(x[kk]));
+  const int e = e8m0_of(amax);
+  const float inv = ldexpf(1.f, 127 - e);
+  // half h gets keys kk with (kk >> 2) & 1 == h, at byte 16u + (kk & 3) + 4 (kk >> 3)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = clampf8(x[(i & 3) + 8 * (i >> 2) + 4 * h] * inv);
+    unsigned char* dst = vt8 + (bt * D + d) * KT + 32 * h + 16 * u;
+    *(u32x4*)dst = u32x4{pk4(y[0], y[1], y[2], y[3]), pk4(y[4], y[5], y[6], y[7]),
+                         pk4(y[8], y[9], y[10], y[11]), pk4(y[12], y[13], y[14], y[15])};
+  }
+  vts[bt * 512 + u * 256 + (d & 31) * 8 + (d >> 5)] = (unsigned char)e;
+}
+
+struct F8Dir {
+  const unsigned char* q8; const unsigned char* qs;    // [B][HWp][256], [B][HWp][8]
+  const unsigned char* k8; const unsigned char* ks;
+  const unsigned char* vt8; const unsigned char* vts;  // [B][nt][256][64], [B][nt][512]
+  bf16* o; long long ldo;
+  float* lse;                                          // optional [B][HWp32] log2-sum-exp2
+};
+struct F8Args {
+  F8Dir dir[2];
+  int HW, HWp, HWp32, nt, ndir, nrb, nitems;
+};
+
+// ---- main kernel ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void coatt_f8_fwd_k(F8Args a) {
+  // [Q 32 KB][Q scales 1 KB][stage 0: K | V^T | scales] x NSTAGE
+  __shared__ __attribute__((aligned(16))) char lds[QBYTES + 1024 + NSTAGE * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // XCD-aware order: each XCD gets a contiguous run of (row block, batch x direction) items
+  const int n8 = (a.nitems + 7) & ~7;
+  const int item = (blockIdx.x & 7) * (n8 >> 3) + (blockIdx.x >> 3);
+  if (item >= a.nitems) return;
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const F8Dir d = a.dir[bd % a.ndir];
+  const long long b = bd / a.ndir;
+  const int HW = a.HW;
+  const int q0 = rb * QB;
+  const unsigned char* Q8 = d.q8 + (b * a.HWp + q0) * D;
+  const unsigned char* Qs = d.qs + (b * a.HWp + q0) * 8;
+  const unsigned char* K8 = d.k8 + b * a.HWp * D;
+  const unsigned char* Ks = d.ks + b * a.HWp * 8;
+  const unsigned char* VT8 = d.vt8 + b * a.nt * VBYTES;
+  const unsigned char* VTs = d.vts + b * a.nt * 512;
+  char* qlds = lds;
+  char* qslds = lds + QBYTES;
+  char* ring = lds + QBYTES + 1024;
+  const int woff = __builtin_amdgcn_readfirstlane((tid & ~63) * 16);   // this wave's DMA window
+
+  // Q image: position p -> row p >> 4, chunk position p & 15, source chunk pos ^ (row & 15)
+#pragma unroll
+  for (int i = 0; i < QBYTES / 4096; ++i) {
+    const int p = i * 256 + tid;
+    const int row = p >> 4, pos = p & 15;
+    glds16(Q8 + row * D + ((pos ^ (row & 15)) << 4), qlds + i * 4096 + woff);
+  }
+  // Q scales (1 KB): each wave fetches 256 B with its first 16 lanes
+  if (lane < 16) glds16(Qs + w * 256 + lane * 16, qslds + w * 256);
+
+  auto issue = [&](int t, int stage) {
+    char* kb = ring + stage * STAGE;
+    char* vb = kb + KBYTES;
+    char* sb = vb + VBYTES;
+    const unsigned char* ksrc = K8 + (long long)t * KT * D;
+    const unsigned char* vsrc = VT8 + (long long)t * VBYTES;
+#pragma unroll
+    for (int i = 0; i < KBYTES / 4096; ++i) {
+      const int p = i * 256 + tid;
+      const int row = p >> 4, pos = p & 15;
+      glds16(ksrc + row * D + ((pos ^ (row & 15)) << 4), kb + i * 4096 + woff);
+    }
+#pragma unroll
+    for (int i = 0; i < VBYTES / 4096; ++i) {
+      const int p = i * 256 + tid;
+      const int row = p >> 2, pos = p & 3;        // V^T rows of 64 B
+      glds16(vsrc + row * KT + ((pos ^ ((row >> 2) & 1)) << 4), vb + i * 4096 + woff);
+    }
+    // scales: waves 0,1 -> K scales (rows of the tile), waves 2,3 -> V^T scales
+    if (lane < 16) {
+      const unsigned char* ss = w < 2 ? Ks + (long long)t * KT * 8 + w * 256
+                                      : VTs + (long long)t * 512 + (w - 2) * 256;
+      glds16(ss + lane * 16, sb + w * 256);
+    }
+  };
+
+  const int nt = a.nt;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+
+  f32x16 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  const float L2E = 1.4426950408889634f;
+  const int qrow = q0 + w * 32 + r;
+  const char* qrp = qlds + (w * 32 + r) * D;
+  const int sw = r & 15;
+  // this lane's Q scales: byte kk of the word = block 2kk + h
+  int qsc = 0;
+
+  int st = 0, st2 = 2;
+  for (int t = 0; t < nt; ++t) {
+    // tile t landed when only tile t+1's NDMA instructions may still be in flight
+    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NDMA) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (t == 0) qsc = *(const int*)(qslds + (w * 32 + r) * 8 + 4 * h);
+    if (t + 2 < nt) issue(t + 2, st2);
+    const char* kb = ring + st * STAGE;
+    const char* vb = kb + KBYTES;
+    const char* sb = vb + VBYTES;
+    st = st == NSTAGE - 1 ? 0 : st + 1;
+    st2 = st2 == NSTAGE - 1 ? 0 : st2 + 1;
+
+    // ---- S^T = K Q^T for the two 32-key halves of the tile (4 MFMA steps of 64 channels)
+    f32x16 s[2] = {f32x16{}, f32x16{}};
+    const int ksc0 = *(const int*)(sb + r * 8 + 4 * h);          // keys r, 32 + r
+    const int ksc1 = *(const int*)(sb + (32 + r) * 8 + 4 * h);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      // bytes 0-15: channels 64kk + 16h + [0,16) (k-block 0), 16-31: + 32 (k-block 1)
+      const int c0 = ((4 * kk + h) ^ sw) << 4, c1 = ((4 * kk + 2 + h) ^ sw) << 4;
+      const u32x4 qa = *(const u32x4*)(qrp + c0), qb = *(const u32x4*)(qrp + c1);
+      const i32x8 qf = {(int)qa.x, (int)qa.y, (int)qa.z, (int)qa.w, (int)qb.x, (int)qb.y, (int)qb.z, (int)qb.w};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const char* krp = kb + (32 * u + r) * D;
+        const u32x4 ka = *(const u32x4*)(krp + c0), kb2 = *(const u32x4*)(krp + c1);
+        const i32x8 kf = {(int)ka.x, (int)ka.y, (int)ka.z, (int)ka.w, (int)kb2.x, (int)kb2.y, (int)kb2.z, (int)kb2.w};
+        const int ks = u ? ksc1 : ksc0;
+        // A = K rows (e4m3, scale per 32-channel block), B = Q^T (e4m3, scale per block)
+        switch (kk) {
+          case 0: s[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s[u], 0, 0, 0, ks, 0, qsc); break;
+          case 1: s[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s[u], 0, 0, 1, ks, 1, qsc); break;
+          case 2: s[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s[u], 0, 0, 2, ks, 2, qsc); break;
+          default: s[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s[u], 0, 0, 3, ks, 3, qsc); break;
+        }
+      }
+    }
+
+    // ---- online softmax over this lane's 32 keys (register i of half u: key
+    // 64t + 32u + (i & 3) + 8 (i >> 2) + 4h)
+    const int key0 = t * KT;
+    if (key0 + KT > HW) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (key0 + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h >= HW) s[u][i] = -INFINITY;
+    }
+    float mx = s[0][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[1][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(m, mx * L2E);
+    if (__builtin_amdgcn_ballot_w64(mnew > m + RESC_T) != 0) {
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      m = mnew;
+    }
+    unsigned pw[8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float p4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p4[e] = __builtin_amdgcn_exp2f(fmaf(s[u][4 * g + e], L2E, -m));
+          l += p4[e];
+        }
+        pw[4 * u + g] = pk4(p4[0], p4[1], p4[2], p4[3]);
+      }
+    const i32x8 pf = {(int)pw[0], (int)pw[1], (int)pw[2], (int)pw[3], (int)pw[4], (int)pw[5], (int)pw[6], (int)pw[7]};
+
+    // ---- O^T += V^T P^T: one scaled MFMA per 32-channel block dt covers the 64 keys
+    const int vs0 = *(const int*)(sb + 512 + h * 256 + r * 8);       // blocks dt 0..3
+    const int vs1 = *(const int*)(sb + 512 + h * 256 + r * 8 + 4);   // blocks dt 4..7
+    const int vsw = (r >> 2) & 1;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const char* vrp = vb + (32 * dt + r) * KT;
+      const u32x4 va = *(const u32x4*)(vrp + (((2 * h) ^ vsw) << 4));
+      const u32x4 vb2 = *(const u32x4*)(vrp + (((2 * h + 1) ^ vsw) << 4));
+      const i32x8 vf = {(int)va.x, (int)va.y, (int)va.z, (int)va.w, (int)vb2.x, (int)vb2.y, (int)vb2.z, (int)vb2.w};
+      const int vsc = dt < 4 ? vs0 : vs1;
+      switch (dt & 3) {   // A = V^T (scale per channel and 32-key half), B = P^T (unit scale)
+        case 0: o[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[dt], 0, 0, 0, vsc, 0, 127); break;
+        case 1: o[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[dt], 0, 0, 1, vsc, 0, 127); break;
+        case 2: o[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[dt], 0, 0, 2, vsc, 0, 127); break;
+        default: o[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[dt], 0, 0, 3, vsc, 0, 127); break;
+      }
+    }
+  }
+
+  // ---- epilogue: O[qrow][d] = o / l ; register i of block dt holds d = 32 dt + (i&3) + 8(i>>2) + 4h
+  l += __shfl_xor(l, 32, 64);
+  if (d.lse && h == 0 && qrow < a.HWp32)
+    d.lse[b * a.HWp32 + qrow] = qrow < HW ? m + __builtin_amdgcn_logf(l) : INFINITY;
+  if (qrow < HW) {
+    const float inv = 1.f / l;
+    bf16* op = d.o + (b * HW + qrow) * d.ldo + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+        *(bf16x4*)(op + 32 * dt + 8 * c) = v;
+      }
+  }
+}
+
+}  // namespace
+
+static inline int hwp64(int HW) { return (HW + KT - 1) / KT * KT; }
+
+// workspace: two row images (Va_t, Vb) + two V^T images (Vb, Va), each with its scales
+extern "C" size_t cn_coatt_f8_workspace_bytes(int B, int HW) {
+  const size_t rows = (size_t)B * hwp64(HW);
+  const size_t nt = (size_t)hwp64(HW) / KT;
+  return 2 * rows * (D + 8) + 2 * (size_t)B * nt * (VBYTES + 512) + 256;
+}
+
+// Z_a, Z_b (bf16) of the co-attention with MX-fp8 operands; lse_a / lse_b (optional, [B][HWp32],
+// HWp32 = ceil32(HW)) as cn_coatt_flash_fwd's, for the bf16 flash backward.
+extern "C" int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                               const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                               void* zb, long long ld_z, float* lse_a, float* lse_b, void* ws,
+                               size_t ws_bytes, hipStream_t st) {
+  if (B <= 0 || HW <= 0 || C != D || !za || !zb) return CN_ERR_SHAPE;
+  if (ld_vat % 8 || ld_va % 8 || ld_vb % 8 || ld_z % 4) return CN_ERR_ALIGN;
+  if (((uintptr_t)vat & 15) || ((uintptr_t)va & 15) || ((uintptr_t)vb & 15) || ((uintptr_t)za & 7) ||
+      ((uintptr_t)zb & 7))
+    return CN_ERR_ALIGN;
+  if (!ws || ((uintptr_t)ws & 255) || ws_bytes < cn_coatt_f8_workspace_bytes(B, HW)) return CN_ERR_SHAPE;
+  const int HWp = hwp64(HW), nt = HWp / KT;
+  const size_t rows = (size_t)B * HWp;
+  unsigned char* p = (unsigned char*)ws;
+  unsigned char* a8 = p;              p += rows * D;
+  unsigned char* b8 = p;              p += rows * D;
+  unsigned char* as = p;              p += rows * 8;
+  unsigned char* bs = p;              p += rows * 8;
+  p = (unsigned char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+  unsigned char* vtb = p;             p += (size_t)B * nt * VBYTES;
+  unsigned char* vta = p;             p += (size_t)B * nt * VBYTES;
+  unsigned char* vtbs = p;            p += (size_t)B * nt * 512;
+  unsigned char* vtas = p;
+  const long long nr = (long long)rows * 8;
+  const dim3 gr((unsigned)((nr + 255) / 256));
+  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vat, ld_vat, B, HW, HWp, a8, as);
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, HWp, b8, bs);
+  CN_CHECK_LAUNCH();
+  const long long nv = (long long)B * nt * 2 * D;
+  const dim3 gv((unsigned)((nv + 255) / 256));
+  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, nt, vtb, vtbs);
+  CN_CHECK_LAUNCH();
+  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)va, ld_va, B, HW, nt, vta, vtas);
+  CN_CHECK_LAUNCH();
+  F8Args a = {};
+  // direction 0: Z_a = softmax_j(S) Vb  (queries Va_t, keys Vb, values Vb)
+  a.dir[0] = F8Dir{a8, as, b8, bs, vtb, vtbs, (bf16*)za, ld_z, lse_a};
+  // direction 1: Z_b = softmax_i(S)^T Va  (queries Vb, keys Va_t, values Va)
+  a.dir[1] = F8Dir{b8, bs, a8, as, vta, vtas, (bf16*)zb, ld_z, lse_b};
+  a.HW = HW; a.HWp = HWp; a.HWp32 = (HW + 31) / 32 * 32; a.nt = nt; a.ndir = 2;
+  a.nrb = (HW + QB - 1) / QB;
+  a.nitems = a.nrb * B * 2;
+  hipLaunchKernelGGL(coatt_f8_fwd_k, dim3((a.nitems + 7) & ~7), dim3(256), 0, st, a);
+  CN_CHECK_LAUNCH();
+  return 0;
+}

@@ -367,7 +367,17 @@ __device__ __forceinline__ void raw_barrier() {
 // BN-epilogue variants of the 128-row tiles keep <= 128 VGPRs (4 waves per SIMD = two 512-thread
 // blocks per CU, the
 // occupancy the plain kernel has from its LDS footprint; HIP's 2nd bound is waves per SIMD).
-template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0>
+//
+// PP (ping-pong, 8 waves, KC bf16 operands only): the waves form two groups of four -- one wave
+// of each group per SIMD -- and group 1 runs one barrier behind group 0, so between any two
+// barriers one group issues its MFMAs (one 32-deep k piece of its wave tile) while the other
+// reads its next fragments and issues the LDS-DMA refill.  Each K step is four barrier phases
+// per group: [frags pc0, refill] | [MFMA pc0] | [frags pc1, counted wait for tile kt+1] |
+// [MFMA pc1].  RAW: every wave's wait for tile kt+1 precedes its third barrier of step kt, and
+// both groups read tile kt+1 only after the barrier that follows the later group's wait.  WAR:
+// a stage is refilled in the first phase of step kt, after the barrier that follows both groups'
+// (lgkmcnt-drained) reads of the tile it held (step kt-1).
+template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0, int PP = 0>
 __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128 && S == 2) ? 4 : 1) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
   constexpr int VEC = VecOf<T>::N;
@@ -576,11 +586,65 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
     wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
     raw_barrier();
   };
-  for (int kt = 0; kt < nt; kt += S) {
-    kstep(kt, std::integral_constant<int, 0>{});
-    if (kt + 1 < nt) kstep(kt + 1, std::integral_constant<int, 1>{});
-    if constexpr (S > 2) { if (kt + 2 < nt) kstep(kt + 2, std::integral_constant<int, (S > 2 ? 2 : 0)>{}); }
-    if constexpr (S > 3) { if (kt + 3 < nt) kstep(kt + 3, std::integral_constant<int, (S > 3 ? 3 : 0)>{}); }
+  constexpr bool PPK = PP && sizeof(T) == 2 && !AMC && !BMC && WM * WN == 8;
+  if constexpr (PPK) {
+    const bool g1 = __builtin_amdgcn_readfirstlane(wave) >= 4;   // waves w, w + 4 share a SIMD
+    auto phase_mma = [&](const bf16x8 (&af)[RM], const bf16x8 (&bfr)[RN]) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+    };
+    auto kstep_pp = [&](int kt, auto stg_c) {
+      constexpr int STG = decltype(stg_c)::value;
+      constexpr int NXT = (STG + S - 1) % S;
+      const char* As = smem + STG * STAGE;
+      const char* Bs = As + ABYTES;
+      {
+        bf16x8 af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, false>(As, wm * TM + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, false>(Bs, wn * TN + j * 16, 0, lane);
+        if (kt + S - 1 < nt) {
+          la.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE, tid);
+          lb.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE + ABYTES, tid);
+        }
+        phase_mma(af, bfr);
+      }
+      {
+        bf16x8 af[RM], bfr[RN];
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, false>(As, wm * TM + i * 16, 1, lane);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, false>(Bs, wn * TN + j * 16, 1, lane);
+        wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
+        phase_mma(af, bfr);
+      }
+    };
+    if (g1) raw_barrier();
+    for (int kt = 0; kt < nt; kt += S) {
+      kstep_pp(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nt) kstep_pp(kt + 1, std::integral_constant<int, 1>{});
+      if constexpr (S > 2) { if (kt + 2 < nt) kstep_pp(kt + 2, std::integral_constant<int, (S > 2 ? 2 : 0)>{}); }
+      if constexpr (S > 3) { if (kt + 3 < nt) kstep_pp(kt + 3, std::integral_constant<int, (S > 3 ? 3 : 0)>{}); }
+    }
+    if (!g1) raw_barrier();
+  } else {
+    for (int kt = 0; kt < nt; kt += S) {
+      kstep(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nt) kstep(kt + 1, std::integral_constant<int, 1>{});
+      if constexpr (S > 2) { if (kt + 2 < nt) kstep(kt + 2, std::integral_constant<int, (S > 2 ? 2 : 0)>{}); }
+      if constexpr (S > 3) { if (kt + 3 < nt) kstep(kt + 3, std::integral_constant<int, (S > 3 ? 3 : 0)>{}); }
+    }
   }
 
   // Epilogue: stage alpha*acc (fp32) through LDS, HR tile rows per pass, as [HR][BN+4]; then
@@ -803,7 +867,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
 // ---------------------------------------------------------------------------------------
 // Tile configurations and dispatch.  grid = (ceil(M/BM), ceil(N/BN), batch * nsplit)
 // ---------------------------------------------------------------------------------------
-struct TileCfg { int bm, bn, wm, wn, s; };
+struct TileCfg { int bm, bn, wm, wn, s, pp; };
 // bf16 configurations (index = config id); fp32 (parity path) always uses id 1's tile with S=2
 static constexpr TileCfg kCfg[] = {
     {128, 64, 2, 2, 2},   // 0: small grids
@@ -824,6 +888,9 @@ static constexpr TileCfg kCfg[] = {
     {256, 128, 4, 2, 3},  // 15
     {128, 64, 4, 2, 4},   // 16
     {64, 128, 2, 4, 2},   // 17: 8 waves of 32x32, for 64-row products (Cout = 64 wgrad)
+    {256, 128, 4, 2, 3, 1},  // 18: ping-pong, 8 waves of 64x64
+    {128, 256, 2, 4, 3, 1},  // 19: ping-pong, 8 waves of 64x64
+    {256, 256, 2, 4, 2, 1},  // 20: ping-pong, 8 waves of 128x64
 };
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 static int g_force_cfg = -1;
@@ -860,7 +927,7 @@ template <class T, class CT, int C, int LA, int LB, int EPI = 0>
 static int launch_c(const GemmArgs& a, int batch, hipStream_t st) {
   constexpr TileCfg c = kCfg[C];
   dim3 grid((a.M + c.bm - 1) / c.bm, (a.N + c.bn - 1) / c.bn, batch * a.nsplit);
-  hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB, EPI>), grid,
+  hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB, EPI, c.pp>), grid,
                      dim3(c.wm * c.wn * 64), 0, st, a);
   CN_CHECK_LAUNCH();
   return 0;
@@ -879,6 +946,9 @@ static int launch_epi(const GemmArgs& a, hipStream_t st) {
       case 11: return launch_c<T, T, 11, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 12: return launch_c<T, T, 12, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 13: return launch_c<T, T, 13, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 18: return launch_c<T, T, 18, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 19: return launch_c<T, T, 19, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 20: return launch_c<T, T, 20, LA, L_KC_DENSE, EPI>(a, 1, st);
       default: return CN_ERR_UNSUPPORTED;
     }
   }
@@ -908,6 +978,17 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 15: return launch_c<T, CT, 15, LA, LB>(a, batch, st);
       case 16: return launch_c<T, CT, 16, LA, LB>(a, batch, st);
       case 17: return launch_c<T, CT, 17, LA, LB>(a, batch, st);
+      case 18: case 19: case 20: {  // ping-pong tiles: k-contiguous operands only
+        constexpr bool kc = LA != L_MC_DENSE && LA != L_MC_CONV && LB != L_MC_DENSE && LB != L_MC_CONV;
+        if constexpr (kc) {
+          const int c = pick_cfg(a, batch);
+          if (c == 18) return launch_c<T, CT, 18, LA, LB>(a, batch, st);
+          if (c == 19) return launch_c<T, CT, 19, LA, LB>(a, batch, st);
+          return launch_c<T, CT, 20, LA, LB>(a, batch, st);
+        } else {
+          return launch_c<T, CT, 11, LA, LB>(a, batch, st);
+        }
+      }
       default: return launch_c<T, CT, 12, LA, LB>(a, batch, st);
     }
   }

@@ -261,7 +261,7 @@ class CoattFn(F):
     summed inside the HIP GEMM epilogues rather than by an autograd add."""
 
     @staticmethod
-    def forward(ctx, va, vb, wsim, geo, link=None):
+    def forward(ctx, va, vb, wsim, geo, link=None, fp8=False):
         n, hw = geo
         c = va.shape[1]
         dt = va.dtype
@@ -276,12 +276,19 @@ class CoattFn(F):
             za = torch.empty((n * hw, c), dtype=dt, device=dev)
             zb = torch.empty((n * hw, c), dtype=dt, device=dev)
             if not _need(ctx):                                                   # inference
-                ops.coatt_fused(vat, va, vb, n, hw, za, zb)                      # :160-170
+                if fp8:   # configs[4]: MX-fp8 affinity and gathers
+                    ops.coatt_f8(vat, va, vb, n, hw, za, zb)                     # :160-170
+                else:
+                    ops.coatt_fused(vat, va, vb, n, hw, za, zb)                  # :160-170
                 return za, zb
-            # training: keep the per-row normalisers; the backward recomputes P from them
+            # training: keep the per-row normalisers; the backward recomputes P from them (in
+            # bf16; with the fp8 forward the normalisers are the fp8 affinity's)
             lse_a = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=dev)
             lse_b = torch.empty_like(lse_a)
-            ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)       # :160-170
+            if fp8:
+                ops.coatt_f8(vat, va, vb, n, hw, za, zb, lse_a, lse_b)          # :160-170
+            else:
+                ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)   # :160-170
             ctx.s = (va, vb, wf, vat, za, zb, lse_a, lse_b)
             ctx.flash = True
             ctx.link = link
@@ -317,7 +324,7 @@ class CoattFn(F):
         P = n * hw
         dv_link = ctx.link.pop("dv", None) if ctx.link is not None else None
         if dza is None and dzb is None:
-            return dv_link, None, None, None, None
+            return dv_link, None, None, None, None, None
         dza = dza.contiguous() if dza is not None else None
         dzb = dzb.contiguous() if dzb is not None else None
         if dza is not None:
@@ -366,7 +373,7 @@ class CoattFn(F):
             ns = max(1, min(64, P // 512))
             ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
                      ldb=ops.ld(va), out=dw, ldc=c, c_mode=0, nsplit=ns)
-        return dva, None, dw, None, None
+        return dva, None, dw, None, None, None
 
     @staticmethod
     def _flash_backward(ctx, dza, dzb):
@@ -382,7 +389,7 @@ class CoattFn(F):
         P = n * hw
         dv_link = ctx.link.pop("dv", None) if ctx.link is not None else None
         if dza is None and dzb is None:
-            return dv_link, None, None, None, None
+            return dv_link, None, None, None, None, None
         dza = dza.contiguous() if dza is not None else None
         dzb = dzb.contiguous() if dzb is not None else None
         need_va = ctx.needs_input_grad[0]
@@ -407,7 +414,7 @@ class CoattFn(F):
             ns = max(1, min(64, P // 512))
             ops.gemm(dvat, va, c, c, P, layout_a=ops.GEMM_MC, layout_b=ops.GEMM_MC, lda=c,
                      ldb=ops.ld(va), out=dw, ldc=c, c_mode=0, nsplit=ns)
-        return dva, None, dw, None, None
+        return dva, None, dw, None, None, None
 
 
 # ==============================================================================================

@@ -442,6 +442,22 @@ def hw_pad(hw):
     return (hw + 31) // 32 * 32
 
 
+def coatt_f8(vat, va, vb, n, hw, za, zb, lse_a=None, lse_b=None):
+    """Both co-attention directions with MX-fp8 operands (BASELINE configs[4]: e4m3 bytes + one
+    E8M0 exponent per 32 reduction values, the block-scaled 32x32x64 MFMA), softmax statistics
+    in fp32; optional per-row log2-sum-exp2 [n, hw_pad(hw)] for the bf16 flash backward."""
+    c = vat.shape[1]
+    ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_f8_fwd", n, hw, c),
+                     (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
+    nws = int(nv.query("cn_coatt_f8_workspace_bytes", n, hw))
+    ws = torch.empty((nws,), dtype=torch.uint8, device=vat.device)
+    nv.call("cn_coatt_f8_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(), ld(vb),
+            n, hw, c, za.data_ptr(), zb.data_ptr(), ld(za), nv.ptr(lse_a), nv.ptr(lse_b),
+            ws.data_ptr(), nws, nv.stream())
+    _prof_end(ev)
+    return za, zb
+
+
 def coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b):
     """Training forward of both co-attention directions (S never in HBM) + the per-row
     log2-sum-exp2 normalisers [n, hw_pad(hw)] the backward recomputes P from."""

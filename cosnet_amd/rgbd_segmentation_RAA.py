@@ -230,7 +230,8 @@ class RGBDSegmentation_RAA(nn.Module):
         n, h, w = geo
         hw = h * w
         link = {}   # V_a's two gradient contributions meet inside CoattFn's backward
-        za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw), link)
+        f8 = getattr(self, "fp8", None) is not None and va.dtype == torch.bfloat16   # configs[4]
+        za, zb = fn.CoattFn.apply(va, vb, self.rgb_similarity_weights.weight, (n, hw), link, f8)
         cat_a = fn.GateCatFn.apply(za, va, self.gate.weight, None, False, link)
         cat_b = fn.GateCatFn.apply(zb, vb, self.gate.weight, None, True)  # mask_b no_grad (:178-182)
         z_a = fn.BNFn.apply(fn.ConvFn.apply(cat_a, self.reduce_channels_A.weight, None, geo, 3, 1, 1, 1),
@@ -244,7 +245,8 @@ class RGBDSegmentation_RAA(nn.Module):
         n, h, w = geo
         hw = h * w
         dlink = {}
-        dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw), dlink)
+        f8 = getattr(self, "_fp8_depth", None) is not None and da.dtype == torch.bfloat16
+        dza, dzb = fn.CoattFn.apply(da, db, self.depth_similarity_weights.weight, (n, hw), dlink, f8)
         dcat_a = fn.GateCatFn.apply(dza, da, self.depth_gate.weight, self.depth_gate.bias, False, dlink)
         dz_a = fn.BNFn.apply(fn.ConvFn.apply(dcat_a, self.depth_reduce_channels.weight, None, geo, 3, 1, 1, 1),
                              self.depth_bn.weight, self.depth_bn.bias, self.depth_bn)

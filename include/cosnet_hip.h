@@ -192,6 +192,18 @@ int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long l
  * za/zb 16-byte aligned, ld_z % 8 == 0.  A NULL / too small / misaligned ws is not an error:
  * the launch then runs unsplit (same result, slower tail). */
 size_t cn_coatt_fused_workspace_bytes(int B, int HW, int ndir);
+/* fp8 co-attention forward (BASELINE configs[4], rgbd_segmentation_RAA.py:160-170 / :213-221):
+ * both directions of cn_coatt_flash_fwd with the affinity S = Va_t Vb^T and the gathers P V on
+ * the block-scaled MFMA v_mfma_scale_f32_32x32x64_f8f6f4 -- operands in MX format (e4m3 + one
+ * E8M0 exponent per 32 reduction values, written by a prepass into ws), P in e4m3 (unit
+ * scale, <= 2^8 under the lazy rescale), softmax max / sum in fp32.  lse_a / lse_b optional
+ * ([B][ceil32(HW)], as cn_coatt_flash_fwd).  ws: cn_coatt_f8_workspace_bytes(B, HW) bytes,
+ * 256-byte aligned.  C == 256. */
+size_t cn_coatt_f8_workspace_bytes(int B, int HW);
+int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                    const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                    long long ld_z, float* lse_a, float* lse_b, void* ws, size_t ws_bytes,
+                    hipStream_t stream);
 int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
                           const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                           long long ld_z, void* ws, size_t ws_bytes, hipStream_t stream);

@@ -44,6 +44,7 @@ def timeit(fn):
 
 alg = 3 * 2.0 * n * hw * hw * c
 t_k = timeit(lambda: ops.coatt_fused(vat, va, vb, n, hw, za, zb))
+t_8 = timeit(lambda: ops.coatt_f8(vat, va, vb, n, hw, za, zb))   # MX-fp8 (configs[4]), incl. prepass
 
 
 def mat():
@@ -63,4 +64,5 @@ t_f = timeit(fused_block)
 print(json.dumps({"n": n, "hw": hw, "fused_kernel_us": t_k * 1e6,
                   "fused_kernel_alg_tflops": alg / t_k / 1e12,
                   "fused_kernel_exec_tflops": alg * 4 / 3 / t_k / 1e12,
+                  "fp8_us": t_8 * 1e6, "fp8_alg_tflops": alg / t_8 / 1e12,
                   "block_fused_us": t_f * 1e6, "block_materialised_us": t_m * 1e6}))
