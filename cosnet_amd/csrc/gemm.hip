@@ -20,6 +20,7 @@
 #include "gemm.h"
 #include "../../include/cosnet_hip.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -372,11 +373,15 @@ __device__ __forceinline__ void raw_barrier() {
 // of each group per SIMD -- and group 1 runs one barrier behind group 0, so between any two
 // barriers one group issues its MFMAs (one 32-deep k piece of its wave tile) while the other
 // reads its next fragments and issues the LDS-DMA refill.  Each K step is four barrier phases
-// per group: [frags pc0, refill] | [MFMA pc0] | [frags pc1, counted wait for tile kt+1] |
-// [MFMA pc1].  RAW: every wave's wait for tile kt+1 precedes its third barrier of step kt, and
-// both groups read tile kt+1 only after the barrier that follows the later group's wait.  WAR:
-// a stage is refilled in the first phase of step kt, after the barrier that follows both groups'
-// (lgkmcnt-drained) reads of the tile it held (step kt-1).
+// per group: [frags pc0] | [MFMA pc0] | [frags pc1, refill, counted wait for tile kt+1] |
+// [MFMA pc1].  A phase's fragment reads are waited for (lgkmcnt) by its MFMA phase, after the
+// barrier, so the read latency overlaps the other group's MFMAs.  RAW: every wave's wait for
+// tile kt+1 precedes its third barrier of step kt, and both groups read tile kt+1 only after the
+// barrier that follows the later group's wait.  WAR: the stage of tile kt-1 is refilled in the
+// third phase of step kt, after the barrier that ends either group's MFMA phase of pc1 of step
+// kt-1 -- the phase whose lgkmcnt wait retired that group's last reads of tile kt-1 (a 2-stage
+// ring refills in the first phase instead, and retires the third phase's reads before its
+// barrier).
 template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0, int PP = 0>
 __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128 && S == 2) ? 4 : 1) void gemm_kernel(GemmArgs p) {
   constexpr int NT = WM * WN * 64;
@@ -590,7 +595,6 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   if constexpr (PPK) {
     const bool g1 = __builtin_amdgcn_readfirstlane(wave) >= 4;   // waves w, w + 4 share a SIMD
     auto phase_mma = [&](const bf16x8 (&af)[RM], const bf16x8 (&bfr)[RN]) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       raw_barrier();
       __builtin_amdgcn_s_setprio(1);
@@ -603,6 +607,10 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
       __builtin_amdgcn_sched_barrier(0);
       raw_barrier();
     };
+    auto refill = [&](int kt, int nxt) {
+      la.issue(kbeg + (kt + S - 1) * BK, smem + nxt * STAGE, tid);
+      lb.issue(kbeg + (kt + S - 1) * BK, smem + nxt * STAGE + ABYTES, tid);
+    };
     auto kstep_pp = [&](int kt, auto stg_c) {
       constexpr int STG = decltype(stg_c)::value;
       constexpr int NXT = (STG + S - 1) % S;
@@ -614,10 +622,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
         for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, false>(As, wm * TM + i * 16, 0, lane);
 #pragma unroll
         for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, false>(Bs, wn * TN + j * 16, 0, lane);
-        if (kt + S - 1 < nt) {
-          la.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE, tid);
-          lb.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE + ABYTES, tid);
-        }
+        if (S == 2 && kt + S - 1 < nt) refill(kt, NXT);
         phase_mma(af, bfr);
       }
       {
@@ -626,7 +631,11 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
         for (int i = 0; i < RM; ++i) af[i] = read_frag_bf16<BM, false>(As, wm * TM + i * 16, 1, lane);
 #pragma unroll
         for (int j = 0; j < RN; ++j) bfr[j] = read_frag_bf16<BN, false>(Bs, wn * TN + j * 16, 1, lane);
+        if (S > 2 && kt + S - 1 < nt) refill(kt, NXT);
         wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
+        // 2-stage ring: the next step's first phase refills this tile's stage, so this phase's
+        // reads must have retired before the barrier (the deeper rings refill two barriers later)
+        if constexpr (S == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         phase_mma(af, bfr);
       }
     };
@@ -910,10 +919,24 @@ static long long cfg_blocks(int c, const GemmArgs& a, int batch) {
 static long long tiles_of(int c, int M, int N) {
   return (long long)((M + kCfg[c].bm - 1) / kCfg[c].bm) * ((N + kCfg[c].bn - 1) / kCfg[c].bn);
 }
+// Round 3 (profiles/r03_gemm_cold_pingpong*.txt): the ping-pong tiles take the wide deep products
+// (256x256, ASPP / layer-4 3x3: -2..-4 %) and the N = 256 frame-pair products with K >= 1024
+// (128x256: layer-3 3x3 fwd -7 %, 1x1 1024->256 fwd -9 %); 256x256 (8 waves of 64x128) also
+// takes the shallow N >= 1024 products (256->1024 fwd -7 %).  Transposed-operand (MC) products
+// picked for a ping-pong tile run its plain twin (launch_tile).  CN_GEMM_HEUR=1 selects the
+// round-2 rules (A/B runs).
 static int heuristic_cfg(int M, int N, int K, int bz) {
+  static const int v1 = [] { const char* e = getenv("CN_GEMM_HEUR"); return e && e[0] == '1'; }();
   if (N <= 64) return 12;
-  if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 10;
+  if (v1) {
+    if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 10;
+    if (tiles_of(11, M, N) * bz <= 256 && K >= 512) return 13;
+    return 11;
+  }
+  if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 20;
   if (tiles_of(11, M, N) * bz <= 256 && K >= 512) return 13;
+  if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return 19;
+  if (N >= 1024 && K <= 512 && tiles_of(10, M, N) * bz >= 200) return 10;
   return 11;
 }
 
@@ -986,6 +1009,7 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
           if (c == 19) return launch_c<T, CT, 19, LA, LB>(a, batch, st);
           return launch_c<T, CT, 20, LA, LB>(a, batch, st);
         } else {
+          if (pick_cfg(a, batch) == 20) return launch_c<T, CT, 10, LA, LB>(a, batch, st);
           return launch_c<T, CT, 11, LA, LB>(a, batch, st);
         }
       }
