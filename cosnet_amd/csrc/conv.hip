@@ -270,9 +270,20 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
     // do not waste half their MFMAs: 128x64 for N <= 64, 64x128 for Cout <= 64
     *cfg = NN <= 64 ? 12 : (M <= 64 ? 17 : 11);
     tiles = cn_gemm_cfg_blocks(*cfg, M, NN);
-    // split target from tools/wgrad_target_sweep.sh: many tiles (ASPP) -> 1024 blocks;
-    // wide Cout with few tiles (layer 3/4) -> 256 (longer K per split); narrow layers -> 512
-    if (target == 512) target = tiles >= 256 ? 1024 : (M >= 256 ? 256 : 512);
+    // split count from a per-split sweep on the step's shapes (tools/wgrad_bench.py,
+    // profiles/r03_wgrad_splits.txt): up to 512 blocks = two co-resident blocks per CU, never a
+    // third round (layer-3 3x3: 8 -> 14 splits 44.6 -> 37.0 us, layer-4 3x3: 2 -> 3 splits
+    // 117.7 -> 91.6 us, layer-3 1x1: 15 -> 28 splits -4 %); many tiles (ASPP) -> 2 per tile
+    if (target == 512) {
+      if (tiles >= 256) target = 1024;
+      else {
+        long long s = 512 / tiles;
+        long long maxs = K / (8 * BK);
+        if (s > maxs) s = maxs;
+        if (s < 1) s = 1;
+        target = (int)(s * tiles);   // want = ceil(target / tiles) = s below
+      }
+    }
   } else {
     *cfg = -1;
     tiles = (long long)((M + 127) / 128) * ((NN + 63) / 64);

@@ -50,6 +50,10 @@ CONV_CASES = [
     (1, 64, 9, 9, 512, 3, 1, 6, 6),
     (1, 320, 5, 6, 256, 3, 1, 1, 1),
     (3, 16, 4, 4, 8, 3, 1, 1, 1),
+    # output rows longer than one K tile: the weight gradient's row-aligned K (gemm.h ConvGeom::kt)
+    # walks several tiles per row, the later ones starting mid-row
+    (2, 16, 6, 150, 32, 3, 1, 1, 1),
+    (1, 8, 5, 141, 16, 3, 2, 1, 1),
 ]
 
 
