@@ -51,6 +51,8 @@ _SIGS = {
     "cn_bn_apply": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P, _P, _L, _P]),
     "cn_bn_apply_fp8": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P,
                              _P, _L, _P, _L, _P, _P]),
+    "cn_bn_apply_ex": (_I, [_I, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _I, _P,
+                            _P, _L, _P, _L, _P, _P, _L, _P]),
     "cn_bn_set_tuning": (_I, [_I, _I]),
     "cn_bn_bwd": (_I, [_I, _P, _L, _P, _L, _P, _L, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _L, _P, _L, _P, _P]),
     "cn_coatt_workspace_floats": (_S, [_I, _I, _I]),

@@ -343,7 +343,8 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
                                                   const float* rgamma, const float* rbeta, int act,
                                                   const float* prelu, T* __restrict__ y,
                                                   long long ldy, unsigned char* __restrict__ y8,
-                                                  long long ldy8, float* qstate) {
+                                                  long long ldy8, float* qstate,
+                                                  unsigned char* __restrict__ mk, long long ldm) {
   constexpr int V = VecOf<T>::N;
   const Layout L = layout_of<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
@@ -403,7 +404,16 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         else if (act == 2) t = t > 0.f ? t : a * t;
         f[u][v] = t;
       }
-      st_chunk(y + r * ldy + c0, f[u]);
+      const u32x4 pk = Chunk<T>::pack(f[u]);
+      *(u32x4*)(y + r * ldy + c0) = pk;
+      if (mk) {  // ReLU mask of the STORED values, one bit per channel (the backward's act 4)
+        float sv[V];
+        Chunk<T>::unpack(pk, sv);
+        unsigned bits = 0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) bits |= (sv[v] > 0.f ? 1u : 0u) << v;
+        mk[r * ldm + chunk] = (unsigned char)bits;
+      }
       if (y8) {  // fp8 copy of the output for an fp8 consumer conv (delayed scaling)
 #pragma unroll
         for (int v = 0; v < V; ++v) qmax = fmaxf(qmax, fabsf(f[u][v]));
@@ -422,10 +432,12 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
 
 // ---- backward reduce: planes sum(dz), sum(dz * xhat) [, sum(dz * pre * (pre<=0)) PReLU] ----
 // dz = dy * mask, mask = (y > 0) for act 1, 1 for act 0, (pre > 0 ? 1 : a) for act 2.
+// act 4: the ReLU mask comes as bits (bn_apply_k's mask output): mk[row * ldm + chunk], bit v.
 template <class T, int NQ>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, long long ldx,
                                                        const T* __restrict__ dy, long long lddy,
                                                        const T* __restrict__ y, long long ldy,
+                                                       const unsigned char* __restrict__ mk,
                                                        int P, int C, const float* mean,
                                                        const float* invstd, const float* gamma,
                                                        const float* beta, int act,
@@ -452,6 +464,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
     const int step = gridDim.y * L.RPB;
     for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
       float xf[UNR][V], d[UNR][V], yf[UNR][V];
+      unsigned mb[UNR];
       // loads issued unconditionally (rows past P re-read row 0 and contribute zero); the
       // activation branch sits outside the unrolled loop so no branch separates the loads
       if (act == 1) {
@@ -461,6 +474,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
           ld_chunk(x + (long long)r * ldx + c0, xf[u]);
           ld_chunk(dy + (long long)r * lddy + c0, d[u]);
           ld_chunk(y + (long long)r * ldy + c0, yf[u]);
+        }
+      } else if (act == 4) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int r = r0 + u * step < P ? r0 + u * step : 0;
+          ld_chunk(x + (long long)r * ldx + c0, xf[u]);
+          ld_chunk(dy + (long long)r * lddy + c0, d[u]);
+          mb[u] = mk[(long long)r * ldy + chunk];
         }
       } else {
 #pragma unroll
@@ -477,6 +498,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const T* __restrict__ x, 
         for (int v = 0; v < V; ++v) {
           float dd = (!in || (act == 1 && !(yf[u][v] > 0.f))) ? 0.f : d[u][v];
           if (act == 3 && !(fmaf(xf[u][v], sc[v], sf[v]) > 0.f)) dd = 0.f;
+          if (act == 4 && !((mb[u] >> v) & 1u)) dd = 0.f;
           float xh = (xf[u][v] - mu[v]) * is[v];
           if (NQ > 2) {
             float pre = fmaf(xh, g[v], b[v]);
@@ -510,6 +532,7 @@ template <class T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, long long ldx,
                                                       const T* __restrict__ dy, long long lddy,
                                                       const T* __restrict__ y, long long ldy,
+                                                      const unsigned char* __restrict__ mk,
                                                       int P, int C, const float* mean,
                                                       const float* invstd, const float* gamma,
                                                       const float* beta, int act,
@@ -542,6 +565,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
   const int step = gridDim.y * L.RPB;
   for (int r0 = blockIdx.y * L.RPB + ty; r0 < P; r0 += UNR * step) {
     float xf[UNR][V], d[UNR][V], yf[UNR][V];
+    unsigned mb[UNR];
     // loads issued unconditionally (rows past P re-read row 0 and are not stored); the
     // activation branch sits outside the unrolled loop so no branch separates the loads
     if (act == 1) {
@@ -551,6 +575,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
         ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
         ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
         ld_chunk(y + (long long)r * ldy + chunk * V, yf[u]);
+      }
+    } else if (act == 4) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * step < P ? r0 + u * step : 0;
+        ld_chunk(x + (long long)r * ldx + chunk * V, xf[u]);
+        ld_chunk(dy + (long long)r * lddy + chunk * V, d[u]);
+        mb[u] = mk[(long long)r * ldy + chunk];
       }
     } else {
 #pragma unroll
@@ -569,6 +601,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
       for (int v = 0; v < V; ++v) {
         float dd = (act == 1 && !(yf[u][v] > 0.f)) ? 0.f : d[u][v];
         if (act == 3 && !(fmaf(xf[u][v], k1[v], sf[v]) > 0.f)) dd = 0.f;
+        if (act == 4 && !((mb[u] >> v) & 1u)) dd = 0.f;
         float xh = (xf[u][v] - mu[v]) * is[v];
         if (act == 2) {
           float pre = fmaf(xh, g[v], b[v]);
@@ -704,13 +737,13 @@ extern "C" int cn_bn_bwd_apply(int dtype, const void* x, long long ldx, const vo
   if (dtype == DT_BF16) {
     gy = grid_rows<bf16>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
     hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
-                       (const bf16*)dy, lddy, (const bf16*)nullptr, 0ll, P, C, mean, invstd, gamma,
+                       (const bf16*)dy, lddy, (const bf16*)nullptr, 0ll, (const unsigned char*)nullptr, P, C, mean, invstd, gamma,
                        beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (bf16*)dx, lddx,
                        (bf16*)nullptr, 0ll);
   } else {
     gy = grid_rows<float>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
     hipLaunchKernelGGL(bn_bwd_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
-                       (const float*)dy, lddy, (const float*)nullptr, 0ll, P, C, mean, invstd, gamma,
+                       (const float*)dy, lddy, (const float*)nullptr, 0ll, (const unsigned char*)nullptr, P, C, mean, invstd, gamma,
                        beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (float*)dx, lddx,
                        (float*)nullptr, 0ll);
   }
@@ -750,7 +783,20 @@ extern "C" int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, i
                                const float* rgamma, const float* rbeta, int act, const float* prelu,
                                void* y, long long ldy, void* y8, long long ldy8, float* qstate,
                                hipStream_t st) {
+  return cn_bn_apply_ex(dtype, x, ldx, P, nseg, C, mean, invstd, gamma, beta, res, ldr, xr, ldxr,
+                        rmean, rinvstd, rgamma, rbeta, act, prelu, y, ldy, y8, ldy8, qstate, nullptr,
+                        0, st);
+}
+
+extern "C" int cn_bn_apply_ex(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                              const float* mean, const float* invstd, const float* gamma,
+                              const float* beta, const void* res, long long ldr, const void* xr,
+                              long long ldxr, const float* rmean, const float* rinvstd,
+                              const float* rgamma, const float* rbeta, int act, const float* prelu,
+                              void* y, long long ldy, void* y8, long long ldy8, float* qstate,
+                              unsigned char* mask, long long ldm, hipStream_t st) {
   if (y8 && (dtype != DT_BF16 || !qstate || ldy8 % 16 || ((uintptr_t)y8 & 7))) return CN_ERR_ALIGN;
+  if (mask && ldm < C / (dtype == DT_BF16 ? 8 : 4)) return CN_ERR_SHAPE;
   const int vec = dtype == DT_BF16 ? 8 : 4;
   if (C % vec || ldx % vec || ldy % vec || (res && ldr % vec) || (xr && ldxr % vec)) return CN_ERR_ALIGN;
   if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
@@ -763,13 +809,13 @@ extern "C" int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, i
     hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy, nseg), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
                        rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy, (unsigned char*)y8, ldy8,
-                       qstate);
+                       qstate, mask, ldm);
   } else {
     gy = grid_rows<float>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
     hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy, nseg), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
                        rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy,
-                       (unsigned char*)nullptr, 0ll, (float*)nullptr);
+                       (unsigned char*)nullptr, 0ll, (float*)nullptr, mask, ldm);
   }
   CN_CHECK_LAUNCH();
   return 0;
@@ -783,22 +829,25 @@ static int bn_bwd_launch(const T* x, long long ldx, const T* dy, long long lddy,
                          T* dres, long long lddres, float* ws, hipStream_t st) {
   int gx, gy = bwd_splits<T>(P, C, &gx);
   const dim3 fin((C + FCH - 1) / FCH);
+  // act 4: `y` is the ReLU bit mask (bytes, row stride ldy) written by cn_bn_apply_ex
+  const unsigned char* mk = act == 4 ? (const unsigned char*)y : nullptr;
+  if (act == 4) y = nullptr;
   if (act == 2) {
     hipLaunchKernelGGL((bn_bwd_reduce_k<T, 3>), dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy,
-                       P, C, mean, invstd, gamma, beta, act, prelu, ws);
+                       mk, P, C, mean, invstd, gamma, beta, act, prelu, ws);
     CN_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_bwd_finalize<3>, fin, dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
   } else {
     hipLaunchKernelGGL((bn_bwd_reduce_k<T, 2>), dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy,
-                       P, C, mean, invstd, gamma, beta, act, prelu, ws);
+                       mk, P, C, mean, invstd, gamma, beta, act, prelu, ws);
     CN_CHECK_LAUNCH();
     hipLaunchKernelGGL(bn_bwd_finalize<2>, fin, dim3(256), 0, st, ws, gy, C, dbeta, dgamma, dprelu_c);
   }
   CN_CHECK_LAUNCH();
   if (!dx) return 0;
   gy = grid_rows<T>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
-  hipLaunchKernelGGL(bn_bwd_apply_k<T>, dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy, P, C,
-                     mean, invstd, gamma, beta, act, prelu, dbeta, dgamma, dx, lddx, dres, lddres);
+  hipLaunchKernelGGL(bn_bwd_apply_k<T>, dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy, mk, P,
+                     C, mean, invstd, gamma, beta, act, prelu, dbeta, dgamma, dx, lddx, dres, lddres);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -810,9 +859,10 @@ extern "C" int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy
                          void* dx, long long lddx, void* dres, long long lddres, float* ws,
                          hipStream_t st) {
   const int vec = dtype == DT_BF16 ? 8 : 4;
-  if (C % vec || ldx % vec || lddy % vec || (y && ldy % vec) || (dx && lddx % vec) ||
+  if (C % vec || ldx % vec || lddy % vec || (y && act != 4 && ldy % vec) || (dx && lddx % vec) ||
       (dres && lddres % vec))
     return CN_ERR_ALIGN;
+  if (act == 4 && (!y || ldy < C / vec)) return CN_ERR_SHAPE;
   if (!aligned16(mean) || !aligned16(invstd) || !aligned16(gamma) || !aligned16(beta) ||
       !aligned16(dgamma) || !aligned16(dbeta))
     return CN_ERR_ALIGN;

@@ -101,23 +101,24 @@ def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=
 
 
 def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None,
-              fp8_key=None):
+              fp8_key=None, mask=None):
     """BN apply; in fp8 mode with fp8_key (the output feeds fp8 convs) also the e4m3 copy of the
-    output in the same pass (delayed scaling; a first use calibrates by a separate pass)."""
+    output in the same pass (delayed scaling; a first use calibrates by a separate pass); with
+    mask (ops.relu_mask) also the ReLU mask bits the backward reads instead of the output."""
     rs = None if rstats is None else (rstats.mean, rstats.invstd)
     ctx = getattr(bn, "_cn_fp8", None)
     if fp8_key is None or ctx is None or x.dtype != torch.bfloat16:
         return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
-                        rstats=rs, rbn=rbn, out=out, nseg=stats.nseg)
+                        rstats=rs, rbn=rbn, out=out, nseg=stats.nseg, mask=mask)
     st = ctx.acts.ready(fp8_key, x.device)
     if st is None:
         y = bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
-                     rstats=rs, rbn=rbn, out=out, nseg=stats.nseg)
+                     rstats=rs, rbn=rbn, out=out, nseg=stats.nseg, mask=mask)
         ctx.acts.quant(y, fp8_key)
         return y
     y8 = torch.empty(tuple(x.shape), dtype=torch.uint8, device=x.device)
     y = bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr, rstats=rs,
-                 rbn=rbn, out=out, nseg=stats.nseg, out8=y8, qstate=st)
+                 rbn=rbn, out=out, nseg=stats.nseg, out8=y8, qstate=st, mask=mask)
     ctx.acts.register(y, y8, st)
     return y
 
@@ -212,35 +213,39 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     c3, _, _, st3 = conv_bn(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1, blk.bn3, tr, nseg,
                             weight=blk.conv3.weight)
     cd = std = wdt = None
+    # the backward of the residual BN + ReLU needs only y > 0: kept as bits (1/16 of y's bytes),
+    # read by bn_bwd(act=4) instead of y (deeplab/residual_net.py:107-109)
+    mk = ops.relu_mask(c3.shape[0], 4 * planes, c3) if rec is not None else None
     if blk.downsample is not None:
         wdf, wdt = WCACHE.get(blk.downsample[0].weight, dt)
         bnd = blk.downsample[1]
         cd, _, _, std = conv_bn(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1, bnd, tr, nseg,
                                 weight=blk.downsample[0].weight)
-        y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd, fp8_key=("out", id(blk)))
+        y = seg_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd, fp8_key=("out", id(blk)),
+                      mask=mk)
     else:
-        y = seg_apply(c3, st3, blk.bn3, act=1, res=x, fp8_key=("out", id(blk)))
+        y = seg_apply(c3, st3, blk.bn3, act=1, res=x, fp8_key=("out", id(blk)), mask=mk)
     if rec is not None:
-        rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt),
+        rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt),
                     (n // nseg, h, w, oh, ow, s, d, planes, x.shape[1])))
     return y, (n, oh, ow)
 
 
 def bottleneck_bwd(item, dy, grads, need_dx=True):
     _, blk, sv, (n, h, w, oh, ow, s, d, planes, cin) = item
-    x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt = sv
+    x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt = sv
     pi, po = n * h * w, n * oh * ow                     # frame-a rows in / out
-    x, c1, y1, c2, y2, c3, y = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], y[:po]
+    x, c1, y1, c2, y2, c3, mk = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], mk[:po]
     has_down = cd is not None
     dx = None
     g3o, b3o = grads.buf(blk.bn3.weight, 4 * planes), grads.buf(blk.bn3.bias, 4 * planes)
     if has_down:
         cd = cd[:po]
-        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dgamma=g3o, dbeta=b3o)
-        dcd, _, _, _ = bn_bwd(cd, dy, y, std[0], blk.downsample[1], act=1)
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, mk, st3[0], blk.bn3, act=4, dgamma=g3o, dbeta=b3o)
+        dcd, _, _, _ = bn_bwd(cd, dy, mk, std[0], blk.downsample[1], act=4)
     else:
         dx = torch.empty_like(x)
-        dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3[0], blk.bn3, act=1, dres=dx, dgamma=g3o, dbeta=b3o)
+        dc3, dg3, db3, _ = bn_bwd(c3, dy, mk, st3[0], blk.bn3, act=4, dres=dx, dgamma=g3o, dbeta=b3o)
     dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1,
                      dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
     # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where

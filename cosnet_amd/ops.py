@@ -566,21 +566,28 @@ def _affine(bn):
     return None, None
 
 
+def relu_mask(p, c, like):
+    """Bit-mask buffer for bn_apply(mask=...): [p, c / vec] bytes (vec = channels per 16-B chunk)."""
+    vec = 8 if like.dtype == torch.bfloat16 else 4
+    return torch.empty((p, c // vec), dtype=torch.uint8, device=like.device)
+
+
 def bn_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, rbn=None, out=None,
-             nseg=1, out8=None, qstate=None):
+             nseg=1, out8=None, qstate=None, mask=None):
     """y = act(bn(x) [+ res] [+ rbn(xr)]) with per-segment statistics ([nseg*C] each); with
-    out8 / qstate also an fp8 copy of y (delayed scaling, amax collected into qstate)."""
+    out8 / qstate also an fp8 copy of y (delayed scaling, amax collected into qstate); with mask
+    (relu_mask) also y > 0 as bits, which bn_bwd(act=4) takes instead of y."""
     p, c = x.shape
     if out is None:
         out = torch.empty((p, c), dtype=x.dtype, device=x.device)
     g, b = _affine(bn)
     rg, rb = _affine(rbn) if rbn is not None else (None, None)
-    nv.call("cn_bn_apply_fp8", dtc(x), x.data_ptr(), ld(x), p // nseg, nseg, c, stats[0].data_ptr(),
+    nv.call("cn_bn_apply_ex", dtc(x), x.data_ptr(), ld(x), p // nseg, nseg, c, stats[0].data_ptr(),
             stats[1].data_ptr(), nv.ptr(g), nv.ptr(b), nv.ptr(res), ld(res) if res is not None else 0,
             nv.ptr(xr), ld(xr) if xr is not None else 0, nv.ptr(rstats[0] if rstats else None),
             nv.ptr(rstats[1] if rstats else None), nv.ptr(rg), nv.ptr(rb), act, nv.ptr(prelu),
             out.data_ptr(), ld(out), nv.ptr(out8), ld(out8) if out8 is not None else 0,
-            nv.ptr(qstate), nv.stream())
+            nv.ptr(qstate), nv.ptr(mask), mask.stride(0) if mask is not None else 0, nv.stream())
     return out
 
 
@@ -589,7 +596,8 @@ def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=N
     """Train-mode BN backward (+ fused activation mask).  Returns dx, dgamma, dbeta, dprelu
     (dgamma / dbeta / dprelu written into the given buffers if any, e.g. gradient-arena slices).
     act=1 with y=None: the ReLU mask is recomputed from x with the forward's affine (no read of
-    the activation; only valid when y = relu(bn(x)) had no residual added)."""
+    the activation; only valid when y = relu(bn(x)) had no residual added).  act=4: y is the
+    bit mask bn_apply(mask=...) wrote (1/16 of y's bytes)."""
     p, c = x.shape
     if act == 1 and y is None:
         act = 3
@@ -603,7 +611,7 @@ def bn_bwd(x, dy, y, stats, bn, act=0, prelu=None, want_dx=True, dx=None, dres=N
     ws = _ws(x.dtype, p, c, x.device)
     g, b = _affine(bn)
     nv.call("cn_bn_bwd", dtc(x), x.data_ptr(), ld(x), dy.data_ptr(), ld(dy), nv.ptr(y),
-            ld(y) if y is not None else 0, p, c, stats[0].data_ptr(), stats[1].data_ptr(), nv.ptr(g),
+            (y.stride(0) if act == 4 else ld(y)) if y is not None else 0, p, c, stats[0].data_ptr(), stats[1].data_ptr(), nv.ptr(g),
             nv.ptr(b), act, nv.ptr(prelu), dgamma.data_ptr(), dbeta.data_ptr(), nv.ptr(dpc),
             nv.ptr(dx), ld(dx) if dx is not None else 0, nv.ptr(dres),
             ld(dres) if dres is not None else 0, ws.data_ptr(), nv.stream())

@@ -153,9 +153,22 @@ int cn_bn_apply_fp8(int dtype, const void* x, long long ldx, int P, int nseg, in
                     const float* rmean, const float* rinvstd, const float* rgamma,
                     const float* rbeta, int act, const float* prelu, void* y, long long ldy,
                     void* y8, long long ldy8, float* qstate, hipStream_t stream);
+/* cn_bn_apply_fp8 that also writes the ReLU mask of the stored y as bits (mask: bytes
+ * [nseg*P][ldm >= C / (8 bf16 | 4 fp32)], bit v of byte c/vec = y[., c] > 0), which cn_bn_bwd takes
+ * with act 4 instead of re-reading y (the residual BN + ReLU of each bottleneck,
+ * deeplab/residual_net.py:107-109 backward). */
+int cn_bn_apply_ex(int dtype, const void* x, long long ldx, int P, int nseg, int C,
+                   const float* mean, const float* invstd, const float* gamma, const float* beta,
+                   const void* res, long long ldr, const void* xr, long long ldxr,
+                   const float* rmean, const float* rinvstd, const float* rgamma,
+                   const float* rbeta, int act, const float* prelu, void* y, long long ldy,
+                   void* y8, long long ldy8, float* qstate, unsigned char* mask, long long ldm,
+                   hipStream_t stream);
 /* launch-shape knobs (blocks / rows per thread of each BN pass), for tuning only */
 int cn_bn_set_tuning(int key, int value);
-/* backward of cn_bn_apply w.r.t. x (train mode), masks fused; dres <- dz for the residual */
+/* backward of cn_bn_apply w.r.t. x (train mode), masks fused; dres <- dz for the residual.
+ * act 1: ReLU mask from y; 3: from x with the forward affine (no residual); 4: y is the bit
+ * mask of cn_bn_apply_ex (ldy = its row stride in bytes); 2: PReLU. */
 int cn_bn_bwd(int dtype, const void* x, long long ldx, const void* dy, long long lddy,
               const void* y, long long ldy, int P, int C, const float* mean, const float* invstd,
               const float* gamma, const float* beta, int act, const float* prelu, float* dgamma,

@@ -200,6 +200,21 @@ def test_batchnorm_residual_forms(cuda, dt):
     torch.cuda.synchronize()
     close(nchw(y1, n, h, w), F.relu(ref_bn(x, bn) + res), dt)
     close(nchw(y2, n, h, w), F.relu(ref_bn(x, bn) + ref_bn(xd, bnd)), dt)
+    # ReLU mask bits written by the apply (the bottleneck's residual BN): exactly y > 0 of the
+    # stored values, and the backward from the bits (act 4) bitwise equal to the one re-reading y
+    mk = ops.relu_mask(xg.shape[0], c, xg)
+    y3 = ops.bn_apply(xg, st, bn, act=1, res=rg, mask=mk)
+    vec = 8 if dt == torch.bfloat16 else 4
+    bits = torch.stack([(mk.long() >> v) & 1 for v in range(vec)], dim=2).reshape(xg.shape[0], c)
+    torch.cuda.synchronize()
+    assert torch.equal(y3, y1) and torch.equal(bits.bool(), y1 > 0)
+    gy = rnd((n, c, h, w), dt, 19)
+    gyg = nhwc(gy).to(dt).to(cuda).contiguous()
+    dres1, dres4 = torch.empty_like(xg), torch.empty_like(xg)
+    d1 = ops.bn_bwd(xg, gyg, y1, st, bn, act=1, dres=dres1)
+    d4 = ops.bn_bwd(xg, gyg, mk, st, bn, act=4, dres=dres4)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(d1[:3], d4[:3])) and torch.equal(dres1, dres4)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])

@@ -51,15 +51,18 @@ def child(flt):
         nn = k * k * cin
         bm, bn = (128, 64) if nn <= 64 else ((64, 128) if cout <= 64 else (128, 128))
         tiles = -(-cout // bm) * -(-nn // bn)
-        for sp in splits:
+        cfgs = [int(v) for v in os.environ.get("WGRAD_CFGS", "-1").split(",")]
+        for sp, cf in [(a, b) for a in splits for b in cfgs]:
+            lib.cn_gemm_force_config(cf)
             if sp:
                 t = sp * tiles
                 lib.cn_gemm_set_wgrad_target(t if t != 512 else 511)
             tw = gtime_sets(sets[:1], reps=20)
             tc = gtime_sets(sets)
-            print("%-18s M=%5d N=%6d K=%6d s=%3s | warm %7.1f us  cold %7.1f us  %6.0f TF/s (cold)" %
-                  (name, cout, nn, n * oh * ow, sp or "auto", tw * 1e6, tc * 1e6, fl / tc / 1e12), flush=True)
+            print("%-18s M=%5d N=%6d K=%6d s=%3s c=%3d | warm %7.1f us  cold %7.1f us  %6.0f TF/s (cold)" %
+                  (name, cout, nn, n * oh * ow, sp or "auto", cf, tw * 1e6, tc * 1e6, fl / tc / 1e12), flush=True)
         lib.cn_gemm_set_wgrad_target(512)
+        lib.cn_gemm_force_config(-1)
         del sets
         torch.cuda.empty_cache()
 
