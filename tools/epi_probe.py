@@ -10,7 +10,14 @@ dev = torch.device('cuda:0')
 dt = torch.bfloat16
 SH = {"l3b_1x1": (8, 256, 60, 60, 1024, 1, 1, 0, 1), "l3_1x1": (8, 1024, 60, 60, 256, 1, 1, 0, 1),
       "l3": (8, 256, 60, 60, 256, 3, 1, 2, 2), "aspp": (8, 2048, 60, 60, 512, 3, 1, 12, 12),
-      "l1_1x1": (8, 256, 119, 119, 64, 1, 1, 0, 1)}
+      "l1_1x1": (8, 256, 119, 119, 64, 1, 1, 0, 1),
+      # round 3: every other conv -> BN shape of the two encoders (frame batch 2 x 4)
+      "l1b_1x1": (8, 64, 119, 119, 256, 1, 1, 0, 1), "l1_3x3": (8, 64, 119, 119, 64, 3, 1, 1, 1),
+      "l1_ds": (8, 64, 119, 119, 256, 1, 1, 0, 1), "l2_1x1": (8, 512, 60, 60, 128, 1, 1, 0, 1),
+      "l2_3x3": (8, 128, 60, 60, 128, 3, 1, 1, 1), "l2b_1x1": (8, 128, 60, 60, 512, 1, 1, 0, 1),
+      "l3_ds": (8, 512, 60, 60, 1024, 1, 1, 0, 1), "l4_1x1": (8, 2048, 60, 60, 512, 1, 1, 0, 1),
+      "l4": (8, 512, 60, 60, 512, 3, 1, 4, 4), "l4b_1x1": (8, 512, 60, 60, 2048, 1, 1, 0, 1),
+      "l4_ds": (8, 1024, 60, 60, 2048, 1, 1, 0, 1)}
 
 
 def tm(fn, reps=30):
