@@ -342,6 +342,45 @@ extern "C" int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int
   return cn_splitk_reduce_impl(ws, ns, a.slab, a.slab, dw, 0, st);
 }
 
+// G independent weight gradients of one conv shape (the same conv of the bottlenecks of a
+// layer) in ONE launch: blockIdx.z = problem, every block runs the whole K (all pixels), so there
+// is no split-K slab and no reduce launch; dW[g] fp32 [Cout][KH][KW][Cin] written directly.
+// The per-problem launch needs split-K to fill the chip (14-28 splits on the layer-3 shapes);
+// G problems of 36 (3x3) or 16 (1x1) tiles do so on their own.
+extern "C" int cn_conv_wgrad_grouped(int dtype, int G, const void* const* xs, long long ldx, int N,
+                                     int H, int W, int Cin, const void* const* dys, long long lddy,
+                                     int OH, int OW, int Cout, int KH, int KW, int stride, int pad,
+                                     int dil, float* const* dws, hipStream_t st) {
+  if (G < 1 || G > GEMM_MAXG) return CN_ERR_SHAPE;
+  if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
+  GemmArgs a = gemm_defaults();
+  a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
+  a.ka_lim = a.kb_lim = a.K;
+  a.lda = lddy;
+  a.ldb = ldx;
+  a.ldc = a.N;
+  int lb = L_MC_DENSE;
+  if (!(KH == 1 && KW == 1 && stride == 1 && pad == 0)) {
+    lb = L_MC_CONV;
+    a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  }
+  a.ngroup = G;
+  for (int g = 0; g < G; ++g) {
+    a.grp.A[g] = dys[g];
+    a.grp.B[g] = xs[g];
+    a.grp.C[g] = dws[g];
+  }
+  // the first problem's pointers for the loaders' range checks (every problem has this shape)
+  a.A = dys[0]; a.B = xs[0]; a.C = dws[0];
+  if (dtype == DT_BF16) {
+    // 128x128 tiles (8 waves) when the group covers the chip twice at one block per CU-slot
+    // pair, 128x64 otherwise (the 1x1 products of few problems)
+    a.cfg = (long long)cn_gemm_cfg_blocks(11, a.M, a.N) * G >= 384 ? 11 : 12;
+    if (a.M <= 64) a.cfg = 17;
+  }
+  return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);
+}
+
 extern "C" int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                                 int accumulate, hipStream_t st) {
   return cn_splitk_reduce_impl(ws, nsplit, slab, n, out, accumulate, st);

@@ -21,6 +21,16 @@ struct ConvGeom {
   FastDiv div_C, div_KW, div_OW, div_OHW;
 };
 
+// Grouped launch: blockIdx.z = problem g (nsplit 1) takes its A / B / C from these arrays
+// instead of the a_bs / b_bs / c_bs strides (independent products of one shape, e.g. the weight
+// gradients of the bottlenecks of a layer).
+constexpr int GEMM_MAXG = 24;
+struct GemmGroup {
+  const void* A[GEMM_MAXG];
+  const void* B[GEMM_MAXG];
+  void* C[GEMM_MAXG];
+};
+
 struct GemmArgs {
   int M, N, K;
   int ka_lim, kb_lim;          // k validity bound of each operand (zero beyond)
@@ -54,6 +64,8 @@ struct GemmArgs {
   int st_seg_rows;
   const void* br_x; long long br_ldx;
   const float* br_mean; const float* br_invstd; const float* br_gamma; const float* br_beta;
+  int ngroup;                  // > 0: grouped launch (GemmGroup), batch = ngroup, nsplit 1
+  GemmGroup grp;
 };
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);

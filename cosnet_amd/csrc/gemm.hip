@@ -452,8 +452,8 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   const int kend = min(p.K, kbeg + p.k_chunk);
   const int nt = (kend - kbeg + BK - 1) / BK;
 
-  const T* Abase = (const T*)p.A + (long long)batch * p.a_bs;
-  const T* Bbase = (const T*)p.B + (long long)batch * p.b_bs;
+  const T* Abase = p.ngroup ? (const T*)p.grp.A[batch] : (const T*)p.A + (long long)batch * p.a_bs;
+  const T* Bbase = p.ngroup ? (const T*)p.grp.B[batch] : (const T*)p.B + (long long)batch * p.b_bs;
 
   LdA la;
   LdB lb;
@@ -670,7 +670,8 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   float alpha = p.alpha;
   if (p.scale_a) alpha *= *p.scale_a;
   if (p.scale_b) alpha *= *p.scale_b;
-  CT* Cb = (CT*)p.C + (long long)batch * p.c_bs + (p.c_mode == 3 ? (long long)split * p.slab : 0);
+  CT* Cb = (p.ngroup ? (CT*)p.grp.C[batch] : (CT*)p.C + (long long)batch * p.c_bs) +
+           (p.c_mode == 3 ? (long long)split * p.slab : 0);
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
   constexpr int GPR = BN / 8;            // 8-column groups per row
   constexpr int RPP = NT / GPR;          // rows per pass

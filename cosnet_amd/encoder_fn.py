@@ -47,6 +47,40 @@ class GradSink(dict):
         super().__setitem__(p, g)
 
 
+class WgradQueue:
+    """Weight gradients of the bottlenecks, run after the dgrad chain of an encoder backward (or of
+    one data-parallel segment) as grouped launches: the same conv of consecutive bottlenecks has
+    one shape, so G of them form one launch of G x tiles workgroups that each run the whole K --
+    no split-K slabs and no reduce launch -- instead of G split-K launches + G reduces on the
+    critical chain (the bottleneck weight gradients cost 5.1 ms of the 32.9 ms step issued one
+    by one, profiles/r03_skip_wgrad_probe.txt).  The dgrad chain does not wait for them: their
+    inputs (dY of the conv, its saved input) stay referenced here until flush()."""
+
+    def __init__(self):
+        self.jobs = {}
+
+    def add(self, x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
+        if dw is None:
+            dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
+        key = (x.dtype, n, h, w, cin, ops.ld(x), oh, ow, cout, ops.ld(dy), k, stride, pad, dil)
+        self.jobs.setdefault(key, []).append((x, dy, dw))
+        return dw
+
+    def flush(self):
+        for key, jobs in self.jobs.items():
+            _, n, h, w, cin, _, oh, ow, cout, _, k, stride, pad, dil = key
+            # grouped when the group alone gives >= 128 workgroups of 128x64
+            tiles = -(-cout // 128) * -(-(k * k * cin) // 64)
+            for i in range(0, len(jobs), ops.GROUP_MAX):
+                chunk = jobs[i:i + ops.GROUP_MAX]
+                if len(chunk) >= 2 and tiles * len(chunk) >= 128:
+                    ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
+                else:
+                    for x, dy, dw in chunk:
+                        conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw)
+        self.jobs = {}
+
+
 # ---- segment helpers -----------------------------------------------------------------------
 class SegStats:
     """BN statistics of nseg stacked frame segments: mean / invstd [nseg*C]; [i] -> segment i."""
@@ -231,8 +265,11 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     return y, (n, oh, ow)
 
 
-def bottleneck_bwd(item, dy, grads, need_dx=True):
+def bottleneck_bwd(item, dy, grads, need_dx=True, wq=None):
+    """Backward of one bottleneck; with a WgradQueue the four weight gradients are queued (their
+    dW buffers are registered in `grads` now and filled by wq.flush())."""
     _, blk, sv, (n, h, w, oh, ow, s, d, planes, cin) = item
+    wgrad = conv_wgrad if wq is None else wq.add
     x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt = sv
     pi, po = n * h * w, n * oh * ow                     # frame-a rows in / out
     x, c1, y1, c2, y2, c3, mk = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], mk[:po]
@@ -246,24 +283,24 @@ def bottleneck_bwd(item, dy, grads, need_dx=True):
     else:
         dx = torch.empty_like(x)
         dc3, dg3, db3, _ = bn_bwd(c3, dy, mk, st3[0], blk.bn3, act=4, dres=dx, dgamma=g3o, dbeta=b3o)
-    dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1,
-                     dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
+    dw3 = wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1,
+                dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
     # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where
     # that is cheaper (fuse_bwd)
     f8 = getattr(blk.bn2, "_cn_fp8", None)
     dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads,
                                  weight=blk.conv3.weight, ctx=f8)
-    dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
-                     dw=grads.buf(blk.conv2.weight, planes, 9 * planes))
+    dw2 = wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
+                dw=grads.buf(blk.conv2.weight, planes, 9 * planes))
     dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1, grads,
                                  weight=blk.conv2.weight, ctx=f8)
-    dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1,
-                     dw=grads.buf(blk.conv1.weight, planes, cin))
+    dw1 = wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1,
+                dw=grads.buf(blk.conv1.weight, planes, cin))
     if need_dx:
         dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
     if has_down:
-        dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1,
-                         dw=grads.buf(blk.downsample[0].weight, 4 * planes, cin))
+        dwd = wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1,
+                    dw=grads.buf(blk.downsample[0].weight, 4 * planes, cin))
         grads[blk.downsample[0].weight] = as_param_grad(dwd, blk.downsample[0].weight)
         if need_dx:
             conv_dgrad(dcd, n, oh, ow, wdt, cin, 1, s, 0, 1, h, w, out=dx, accumulate=True)
@@ -428,10 +465,12 @@ class EncoderPairFn(F):
         f8 = getattr(ctx.enc, "_cn_fp8", None)
         if f8 is not None:
             f8.grads.begin()
+        wq = WgradQueue()
         dx = aspp_bwd(rec[-1], dfa, grads)
         for item in reversed(rec[1:-1]):
-            dx = bottleneck_bwd(item, dx, grads)
+            dx = bottleneck_bwd(item, dx, grads, wq=wq)
         stem_bwd(rec[0], dx, grads)
+        wq.flush()
         if f8 is not None:
             f8.grads.end()   # advance the gradient scales from this backward's amax
         return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
@@ -482,13 +521,15 @@ class DeferredEncoderBwd:
         f8 = getattr(self.enc, "_cn_fp8", None)
         if f8 is not None and k == 0:
             f8.grads.begin()
+        wq = WgradQueue()     # the segment's weight gradients, grouped at its end (its bucket)
         for it in self.plan[k]:
             if it == "aspp":
                 self.dx = aspp_bwd(rec[-1], self.dfa, grads)
             elif it == "stem":
                 stem_bwd(rec[0], self.dx, grads)
             else:
-                self.dx = bottleneck_bwd(by_blk[it], self.dx, grads)
+                self.dx = bottleneck_bwd(by_blk[it], self.dx, grads, wq=wq)
+        wq.flush()
         if k == len(self.plan) - 1:
             self.rec = self.dfa = self.dx = None
             if f8 is not None:

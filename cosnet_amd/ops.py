@@ -336,6 +336,34 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
     return dw
 
 
+GROUP_MAX = 24       # cn_conv_wgrad_grouped's problem limit (gemm.h GEMM_MAXG)
+
+
+def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil):
+    """Weight gradients of G convs of ONE shape in one launch (cn_conv_wgrad_grouped): jobs =
+    [(x, dy, dw)] with x [n*h*w, cin], dy [n*oh*ow, cout] sharing the row strides, dw fp32
+    [cout, k*k*cin] (written).  No split-K workspace and no reduce launch."""
+    import ctypes
+    g = len(jobs)
+    if not 1 <= g <= GROUP_MAX:
+        raise ValueError("1..%d problems per grouped launch" % GROUP_MAX)
+    x0, dy0, _ = jobs[0]
+    if any(ld(x) != ld(x0) or ld(dy) != ld(dy0) for x, dy, _ in jobs):
+        raise ValueError("grouped weight gradients need equal row strides")
+    xs = (ctypes.c_void_p * g)(*[x.data_ptr() for x, _, _ in jobs])
+    dys = (ctypes.c_void_p * g)(*[dy.data_ptr() for _, dy, _ in jobs])
+    dws = (ctypes.c_void_p * g)(*[dw.data_ptr() for _, _, dw in jobs])
+    es = x0.element_size()
+    fl = 2.0 * n * oh * ow * cout * k * k * cin
+    ev = _prof_start(g * fl, ("wgrad", cout, k * k * cin, n * oh * ow),
+                     g * (es * (n * h * w * cin + n * oh * ow * cout) + 4 * cout * k * k * cin))
+    nv.call("cn_conv_wgrad_grouped", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
+            ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil, ctypes.addressof(dws),
+            nv.stream())
+    _prof_end(ev)
+    return [dw for _, _, dw in jobs]
+
+
 def as_param_grad(dw_flat, weight):
     """[cout, k*k*cin] fp32 (OHWI order) -> gradient shaped/stided like the channels_last param."""
     if weight.dim() == 2:

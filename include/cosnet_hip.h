@@ -52,6 +52,14 @@ size_t cn_conv_wgrad_workspace_floats(int dtype, int N, int OH, int OW, int Cout
 int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                   const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
                   int stride, int pad, int dil, float* dw, float* ws, hipStream_t stream);
+/* G (<= 24) weight gradients of one conv shape in one launch (the same conv of the bottlenecks
+ * of a layer, deeplab/residual_net.py:79-94 backward): xs / dys / dws are HOST arrays of the
+ * problems' device pointers; every workgroup runs the whole K, so no workspace and no reduce
+ * (fixed summation order per problem, bitwise reproducible). */
+int cn_conv_wgrad_grouped(int dtype, int G, const void* const* xs, long long ldx, int N, int H, int W,
+                          int Cin, const void* const* dys, long long lddy, int OH, int OW, int Cout,
+                          int KH, int KW, int stride, int pad, int dil, float* const* dws,
+                          hipStream_t stream);
 /* out[i] (+)= sum_s ws[s*slab + i], s < nsplit  (split-K reduction, fp32) */
 int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                      int accumulate, hipStream_t stream);

@@ -93,6 +93,34 @@ def test_conv_fwd_dgrad_wgrad(cuda, dt, case):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 1, 0, 1), (2, 32, 15, 9, 64, 3, 1, 2, 2),
+                                  (2, 256, 7, 9, 128, 1, 2, 0, 1), (1, 64, 9, 9, 512, 3, 1, 6, 6)])
+def test_conv_wgrad_grouped(cuda, dt, case):
+    """G weight gradients of one conv shape in one launch (the bottlenecks' grouped wgrads, no
+    split-K): each problem against torch fp64; the launch is deterministic."""
+    n, cin, h, w, cout, k, s, p, d = case
+    G = 3
+    oh, ow = ops.out_hw(h, w, k, s, p, d)
+    jobs, refs = [], []
+    for g in range(G):
+        x = rnd((n, cin, h, w), dt, 40 + g)
+        gy = rnd((n, cout, oh, ow), dt, 50 + g)
+        wr = torch.zeros((cout, cin, k, k), dtype=torch.float64, requires_grad=True)
+        F.conv2d(x, wr, None, s, p, d).backward(gy)
+        refs.append(wr.grad)
+        dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=cuda)
+        jobs.append((nhwc(x).to(dt).to(cuda).contiguous(), nhwc(gy).to(dt).to(cuda).contiguous(), dw))
+    ops.conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d)
+    first = [dw.clone() for _, _, dw in jobs]
+    ops.conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d)
+    torch.cuda.synchronize()
+    wp = torch.empty((cout, cin, k, k), device=cuda).contiguous(memory_format=torch.channels_last)
+    for (_, _, dw), f, ref in zip(jobs, first, refs):
+        close(ops.as_param_grad(dw, wp), ref, dt)
+        assert torch.equal(dw, f)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 2), (2, 2)])
 def test_gemm_layouts_batched(cuda, dt, la, lb):
     B, M, N, K = 3, 77, 136, 200
