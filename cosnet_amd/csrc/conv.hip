@@ -373,9 +373,12 @@ extern "C" int cn_conv_wgrad_grouped(int dtype, int G, const void* const* xs, lo
   // the first problem's pointers for the loaders' range checks (every problem has this shape)
   a.A = dys[0]; a.B = xs[0]; a.C = dws[0];
   if (dtype == DT_BF16) {
-    // 128x128 tiles (8 waves) when the group covers the chip twice at one block per CU-slot
-    // pair, 128x64 otherwise (the 1x1 products of few problems)
-    a.cfg = (long long)cn_gemm_cfg_blocks(11, a.M, a.N) * G >= 384 ? 11 : 12;
+    // 256x128 tiles (3-deep ring) when they give >= 160 blocks: every block runs the whole K,
+    // so the larger tile's fewer bytes per FLOP pay wherever the grid still covers most CUs
+    // (layer-3 groups 334 -> 250 us (1x1), 561 -> 471 us (3x3), tools/wgrad_grouped_bench.py,
+    // profiles/r03_wgrad_grouped_cfgs.txt); else 128x128 with a 3-deep ring (the depth
+    // encoder's groups of 5-6 and the layer-4 1x1s: 141 -> 130 us, 159 -> 140 us, 148 -> 130 us)
+    a.cfg = (long long)cn_gemm_cfg_blocks(15, a.M, a.N) * G >= 160 ? 15 : 13;
     if (a.M <= 64) a.cfg = 17;
   }
   return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);

@@ -94,7 +94,8 @@ def test_conv_fwd_dgrad_wgrad(cuda, dt, case):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 1, 0, 1), (2, 32, 15, 9, 64, 3, 1, 2, 2),
-                                  (2, 256, 7, 9, 128, 1, 2, 0, 1), (1, 64, 9, 9, 512, 3, 1, 6, 6)])
+                                  (2, 256, 7, 9, 128, 1, 2, 0, 1), (1, 64, 9, 9, 512, 3, 1, 6, 6),
+                                  (1, 512, 12, 12, 512, 3, 1, 1, 1)])   # 256x128 tiles (>= 160 blocks)
 def test_conv_wgrad_grouped(cuda, dt, case):
     """G weight gradients of one conv shape in one launch (the bottlenecks' grouped wgrads, no
     split-K): each problem against torch fp64; the launch is deterministic."""
