@@ -25,6 +25,9 @@ _S = ctypes.c_size_t
 # name -> (restype, argtypes); stream is always the last argument (void*)
 _SIGS = {
     "cn_conv_fwd": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I, _P]),
+    "cn_conv_fwd_ws": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I,
+                            _P, _S, _P]),
+    "cn_conv_fwd_workspace_floats": (_S, [_I, _I, _I, _I]),
     "cn_conv_dgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _L, _I, _I, _I, _P]),
     "cn_conv_wgrad_workspace_floats": (_S, [_I, _I, _I, _I, _I, _I, _I, _I]),
     "cn_conv_wgrad": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

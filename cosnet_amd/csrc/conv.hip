@@ -58,6 +58,96 @@ extern "C" int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H
   return cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, 1, st);
 }
 
+// ---- deep one-round forward convs: 256x256 tiles split over K -------------------------------
+// A forward conv whose 128x256 grid is a single round (<= 256 blocks) and whose K is deep (the
+// ASPP bottleneck conv: M = 28 800, N = 256, K = 9 x 2560) runs every block through the whole K
+// at the bytes per FLOP of a 128x256 tile.  Split over K, 256x256 tiles give as many blocks at
+// half the operand bytes per FLOP; the fp32 slabs are summed in a fixed order (bitwise
+// reproducible) by a reduce that adds the bias and writes the bf16 output.
+static int fwd_split_plan(int dtype, int M, int N, int K, int* nsplit, int* chunk) {
+  *nsplit = 1; *chunk = K;
+  if (dtype != DT_BF16 || K < 16384 || N > 256 || N % 8) return 0;
+  if (cn_gemm_cfg_blocks(19, M, N) > 256) return 0;
+  const long long b20 = cn_gemm_cfg_blocks(20, M, N);
+  int ns = (int)(256 / b20);
+  if (ns < 2) ns = 2;
+  if (ns > 8) ns = 8;
+  const int bk = 64;
+  const int ch = ((K + ns - 1) / ns + bk - 1) / bk * bk;
+  *nsplit = (K + ch - 1) / ch;
+  *chunk = ch;
+  return *nsplit > 1;
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_bf16_k(const float* __restrict__ ws, int nsplit,
+                                                            long long slab, int M, int N,
+                                                            const float* __restrict__ bias,
+                                                            bf16* __restrict__ y, long long ldy) {
+  const int cpr = N / 8;
+  const long long total = (long long)M * cpr;
+  for (long long t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
+    const int r = (int)(t / cpr), c = (int)(t - (long long)r * cpr) * 8;
+    const float* p = ws + (long long)r * N + c;
+    f32x4 a0 = *(const f32x4*)p, a1 = *(const f32x4*)(p + 4);
+    for (int sp = 1; sp < nsplit; ++sp) {
+      a0 += *(const f32x4*)(p + sp * slab);
+      a1 += *(const f32x4*)(p + sp * slab + 4);
+    }
+    float f[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    if (bias) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) f[v] += bias[c + v];
+    }
+    *(u32x4*)(y + (long long)r * ldy + c) = Chunk<bf16>::pack(f);
+  }
+}
+
+extern "C" size_t cn_conv_fwd_workspace_floats(int dtype, int M, int Cout, int K) {
+  int ns, ch;
+  return fwd_split_plan(dtype, M, Cout, K, &ns, &ch) ? (size_t)ns * M * Cout : 0;
+}
+
+// cn_conv_fwd with a workspace: the deep one-round shapes (fwd_split_plan) run split over K into
+// ws (cn_conv_fwd_workspace_floats floats, 16-byte aligned); every other shape, or a missing /
+// too small workspace, is cn_conv_fwd.
+extern "C" int cn_conv_fwd_ws(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                              const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                              const float* bias, void* y, long long ldy, int OH, int OW, float* ws,
+                              size_t ws_floats, hipStream_t st) {
+  int ns, ch;
+  const int M = N * OH * OW, K = KH * KW * Cin;
+  if (!ws || ((uintptr_t)ws & 15) || ((uintptr_t)y & 15) || ldy % 8 ||
+      !fwd_split_plan(dtype, M, Cout, K, &ns, &ch) || ws_floats < (size_t)ns * M * Cout)
+    return cn_conv_fwd(dtype, x, ldx, N, H, W, Cin, w, Cout, KH, KW, stride, pad, dil, bias, y, ldy,
+                       OH, OW, st);
+  if (Cin % vec_of(dtype) || ldx % vec_of(dtype)) return CN_ERR_ALIGN;
+  if (OH != (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  if (OW != (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1) return CN_ERR_SHAPE;
+  GemmArgs a = gemm_defaults();
+  a.M = M; a.N = Cout; a.K = K;
+  a.ka_lim = a.kb_lim = a.K;
+  a.A = x; a.lda = ldx;
+  a.B = w; a.ldb = a.K;
+  a.C = ws; a.ldc = Cout;
+  a.c_mode = 3;
+  a.nsplit = ns;
+  a.k_chunk = ch;
+  a.slab = (long long)M * Cout;
+  a.cfg = 20;
+  int la = L_KC_CONV;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) la = L_KC_DENSE;
+  else a.ga = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  int rc = cn_gemm_dispatch(a, dtype, 1, la, L_KC_DENSE, 1, st);
+  if (rc) return rc;
+  const long long total = (long long)M * (Cout / 8);
+  long long nb = (total + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  hipLaunchKernelGGL(splitk_reduce_bf16_k, dim3((unsigned)nb), dim3(256), 0, st, ws, ns, a.slab, M,
+                     Cout, bias, (bf16*)y, ldy);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---- conv + BatchNorm epilogues ------------------------------------------------------------
 int cn_bn_tile_stats_impl(const float* ws, long long plane, int mtiles, int BM, int M, int nseg, int C,
                           float* mean, float* invstd, float* run_mean, float* run_var, float momentum,

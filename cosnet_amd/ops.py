@@ -176,10 +176,22 @@ def conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=None, out=None):
     es = x.element_size()
     ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("fwd", n * oh * ow, cout, k * k * cin),
                      es * (n * h * w * cin + cout * k * k * cin + n * oh * ow * cout))
-    nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
-            stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
+    nws = fwd_split_floats(x, n * oh * ow, cout, k * k * cin)
+    if nws:   # deep one-round conv (the ASPP bottleneck): 256x256 tiles split over K
+        ws = torch.empty((nws,), dtype=torch.float32, device=x.device)
+        nv.call("cn_conv_fwd_ws", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k,
+                k, stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, ws.data_ptr(),
+                nws, nv.stream())
+    else:
+        nv.call("cn_conv_fwd", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, wf.data_ptr(), cout, k, k,
+                stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, nv.stream())
     _prof_end(ev)
     return out, oh, ow
+
+
+def fwd_split_floats(x, m, cout, kdim):
+    """Workspace of the split-K forward (cn_conv_fwd_workspace_floats; 0: the shape does not split)."""
+    return int(nv.query("cn_conv_fwd_workspace_floats", dtc(x), m, cout, kdim))
 
 
 def conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg=1, bias=None):
@@ -192,6 +204,10 @@ def conv_fwd_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, nseg=1, bias=None
     if M % nseg or M // nseg <= 1:
         raise ValueError("Expected more than 1 value per channel when training, got input size "
                          "torch.Size([%d, %d, 1, 1])" % (M // nseg, cout))
+    if fwd_split_floats(x, M, cout, k * k * cin):
+        # split over K: the statistics come from their own pass over the reduced output
+        y, oh, ow = conv_fwd(x, n, h, w, wf, cout, k, stride, pad, dil, bias=bias)
+        return y, oh, ow, bn_stats(y, bn, True, nseg)
     out = torch.empty((M, cout), dtype=x.dtype, device=x.device)
     mean = torch.empty((nseg * cout,), dtype=torch.float32, device=x.device)
     invstd = torch.empty_like(mean)

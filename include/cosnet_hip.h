@@ -38,6 +38,17 @@ int cn_conv_fwd(int dtype, const void* x, long long ldx, int N, int H, int W, in
                 const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
                 const float* bias, void* y, long long ldy, int OH, int OW, hipStream_t stream);
 
+/* cn_conv_fwd with a workspace (bf16): a deep conv whose 128x256 grid is one round (the ASPP
+ * bottleneck conv, deeplab/deeplabv3_encoder.py:31-32: K = 9 x 2560) runs on 256x256 tiles
+ * split over K into `ws` fp32 slabs, summed in a fixed order with the bias by a reduce that
+ * writes y.  cn_conv_fwd_workspace_floats(dtype, M = N*OH*OW, Cout, K = KH*KW*Cin) is 0 for every
+ * shape that does not split; those (and a missing / small workspace) run as cn_conv_fwd. */
+size_t cn_conv_fwd_workspace_floats(int dtype, int M, int Cout, int K);
+int cn_conv_fwd_ws(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                   const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
+                   const float* bias, void* y, long long ldy, int OH, int OW, float* ws,
+                   size_t ws_floats, hipStream_t stream);
+
 /* dx = conv2d input-gradient (autograd of the calls above).  stride 1: any kernel;
  * stride 2: 1x1 / pad 0 only (deeplab/residual_net.py:59,129 of layer2 block 0). */
 int cn_conv_dgrad(int dtype, const void* dy, long long lddy, int N, int OH, int OW, int Cout,

@@ -92,6 +92,39 @@ def test_conv_fwd_dgrad_wgrad(cuda, dt, case):
         close(nchw(dx2, n, h, w), 2 * xr.grad, dt)
 
 
+@pytest.mark.parametrize("case", [(2, 2048, 9, 9, 256, 3, 1, 1, 1), (2, 2560, 7, 8, 64, 3, 1, 1, 1)])
+def test_conv_fwd_split_k(cuda, case):
+    """Deep one-round forward convs (the ASPP bottleneck shape class, K >= 16384, Cout <= 256) run
+    on 256x256 tiles split over K + a fixed-order bf16 reduce with the bias; conv_fwd_bn's
+    statistics then come from a pass over the reduced output.  Against torch fp64."""
+    n, cin, h, w, cout, k, s, p, d = case
+    dt = torch.bfloat16
+    x = rnd((n, cin, h, w), dt, 61)
+    wt = rnd((cout, cin, k, k), dt, 62, scale=(2.0 / (cin * k * k)) ** 0.5)
+    b = rnd((cout,), torch.float32, 63)
+    y_ref = F.conv2d(x, wt, b, s, p, d)
+    oh, ow = y_ref.shape[2:]
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    assert ops.fwd_split_floats(xg, n * oh * ow, cout, k * k * cin) > 0
+    wp = wt.float().to(cuda).contiguous(memory_format=torch.channels_last)
+    wf, _ = ops.WCACHE.get(wp, dt)
+    y, _, _ = ops.conv_fwd(xg, n, h, w, wf, cout, k, s, p, d, bias=b.float().to(cuda))
+    y2, _, _ = ops.conv_fwd(xg, n, h, w, wf, cout, k, s, p, d, bias=b.float().to(cuda))
+    torch.cuda.synchronize()
+    close(nchw(y, n, oh, ow), y_ref, dt)
+    assert torch.equal(y, y2)
+    bn = _bn_mod(cout, cuda, 64)
+    yb, _, _, (mean, invstd) = ops.conv_fwd_bn(xg, n, h, w, wf, cout, k, s, p, d, bn, nseg=1,
+                                               bias=b.float().to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(yb, y)
+    yd = nchw(y, n, oh, ow).double().cpu()
+    m_ref = yd.mean(dim=(0, 2, 3))
+    v_ref = yd.var(dim=(0, 2, 3), unbiased=False)
+    assert torch.allclose(mean.double().cpu(), m_ref, rtol=1e-4, atol=1e-4 * m_ref.abs().max().item())
+    assert torch.allclose(invstd.double().cpu(), 1 / torch.sqrt(v_ref + bn.eps), rtol=1e-3)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 1, 0, 1), (2, 32, 15, 9, 64, 3, 1, 2, 2),
                                   (2, 256, 7, 9, 128, 1, 2, 0, 1), (1, 64, 9, 9, 512, 3, 1, 6, 6),
