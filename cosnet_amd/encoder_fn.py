@@ -69,11 +69,13 @@ class WgradQueue:
     def flush(self):
         for key, jobs in self.jobs.items():
             _, n, h, w, cin, _, oh, ow, cout, _, k, stride, pad, dil = key
-            # grouped when the group alone gives >= 128 workgroups of 128x64
+            # grouped when >= 3 problems give >= 128 workgroups of 128x64 (two layer-4 1x1
+            # weight gradients: 2 x 55 us split-K vs 137 us grouped; three: 160 vs 144 us,
+            # profiles/r03_wgrad_l4_1x1.txt)
             tiles = -(-cout // 128) * -(-(k * k * cin) // 64)
             for i in range(0, len(jobs), ops.GROUP_MAX):
                 chunk = jobs[i:i + ops.GROUP_MAX]
-                if len(chunk) >= 2 and tiles * len(chunk) >= 128:
+                if len(chunk) >= 3 and tiles * len(chunk) >= 128:
                     ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
                 else:
                     for x, dy, dw in chunk:

@@ -18,6 +18,8 @@ SHAPES = [
     ("stem_7x7_s2", 4, 8, 473, 473, 64, 7, 2, 3, 1),
     ("l3_1x1_1024to256", 4, 1024, 60, 60, 256, 1, 1, 0, 1),
     ("l3_1x1_256to1024", 4, 256, 60, 60, 1024, 1, 1, 0, 1),
+    ("l4_1x1_2048to512", 4, 2048, 60, 60, 512, 1, 1, 0, 1),
+    ("l4_1x1_512to2048", 4, 512, 60, 60, 2048, 1, 1, 0, 1),
 ]
 
 
