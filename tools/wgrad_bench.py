@@ -11,6 +11,7 @@ SHAPES = [
     ("l3_3x3_d2", 4, 256, 60, 60, 256, 3, 1, 2, 2),
     ("l4_3x3_d4", 4, 512, 60, 60, 512, 3, 1, 4, 4),
     ("aspp_3x3_d12", 4, 2048, 60, 60, 512, 3, 1, 12, 12),
+    ("aspp_bneck_3x3", 4, 2560, 60, 60, 256, 3, 1, 1, 1),
     ("l2_3x3", 4, 128, 60, 60, 128, 3, 1, 1, 1),
     ("l2_3x3_s2", 4, 128, 119, 119, 128, 3, 2, 1, 1),
     ("l1_3x3", 4, 64, 119, 119, 64, 3, 1, 1, 1),
