@@ -53,8 +53,9 @@ class WgradQueue:
     one shape, so G of them form one launch of G x tiles workgroups that each run the whole K --
     no split-K slabs and no reduce launch -- instead of G split-K launches + G reduces on the
     critical chain (the bottleneck weight gradients cost 5.1 ms of the 32.9 ms step issued one
-    by one, profiles/r03_skip_wgrad_probe.txt).  The dgrad chain does not wait for them: their
-    inputs (dY of the conv, its saved input) stay referenced here until flush()."""
+    by one, profiles/r03_skip_wgrad_probe.txt).  They are issued after the chain on the same
+    stream (on a side stream they slowed the chain, profiles/r03_wgrad_side_stream_ab.txt);
+    their inputs (dY of the conv, its saved input) stay referenced here until flush()."""
 
     def __init__(self):
         self.jobs = {}
