@@ -41,6 +41,21 @@ def rocprof_avg_us(substr):
                 "launches": n, "source": os.path.relpath(ROCPROF_FILE, REPO)} if n else None
     except (OSError, KeyError, ValueError):
         return None
+COATT_TRACE_FILE = os.path.join(REPO, "profiles", "r04_coatt_trace.json")
+
+
+def coatt_trace():
+    """Co-attention kernel time per training step / per configs[3] launch from the committed
+    rocprofv3 --kernel-trace summary of this bench command (tools/coatt_trace_summary.py)."""
+    try:
+        with open(COATT_TRACE_FILE) as f:
+            d = json.load(f)
+        d["source"] = os.path.relpath(COATT_TRACE_FILE, REPO) + ": " + d.get("source", "")
+        return d
+    except (OSError, ValueError):
+        return None
+
+
 FLOP_PER_PAIR_473 = 4.1364e12    # SURVEY.md §8d (flop_counter on the reference graph)
 
 
@@ -55,6 +70,9 @@ def parse():
                     help="fp8: e4m3 operands for the encoders' forward conv GEMMs (BASELINE "
                          "configs[4]; bf16 everywhere else)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle (rank 0)")
+    ap.add_argument("--fp32-extra", type=int, default=1,
+                    help="also time a few recorded fp32 steps (full-precision throughput beside "
+                         "the bf16 headline; N = 1 only)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
@@ -182,6 +200,39 @@ def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):
             "achieved": alg / t / 1e12, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": alg / t / 1e12 / MFMA_BF16_PEAK_TFLOPS,
             "executed_tflops": 4 / 3 * alg / t / 1e12, "us_per_launch": t * 1e6}
+
+
+def fp32_extra(dev, B, S, steps=5, warmup=2):
+    """Full-precision throughput beside the bf16 headline: the same recorded train step in fp32
+    (every GEMM on the f32 MFMA, 157 TFLOP/s peak), `steps` timed replays after `warmup`."""
+    import torch
+    import cosnet_amd as C
+    from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
+    from cosnet_amd.optim import SGD, reference_param_groups
+    from cosnet_amd.train_step import TrainStep
+    m = C.build_model(torch.float32)
+    m.load_state_dict(recipe_state_dict(m.state_dict()))
+    m.encoder.main_classifier.requires_grad_(False)
+    m = m.to(dev).train()
+    g0, g1 = reference_param_groups(m)
+    opt = SGD([g0, g1], [2.5e-6, 2.5e-3], momentum=0.9, weight_decay=5e-4)
+    st = TrainStep(m, opt, B, S, graphed=True)
+    st.load(*[t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234)])
+    st.capture(warmup=warmup)
+    st([2.5e-6, 2.5e-3])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = st([2.5e-6, 2.5e-3])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"value": B * steps / dt, "unit": "frame-pairs/s", "dtype": "fp32", "steps": steps,
+           "ms_per_step": dt / steps * 1e3, "loss": float(loss.item()),
+           "model_tflops_per_s": B * steps * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
+           "peak_tflops": MFMA_F32_PEAK_TFLOPS}
+    del st, opt, m
+    torch.cuda.empty_cache()
+    return out
 
 
 def _free_port():
@@ -409,10 +460,25 @@ def main():
                 "achieved": ffl / ft / 1e12, "peak": peak, "unit": "TFLOP/s", "frac": ffl / ft / 1e12 / peak,
                 "launches_per_step": fn_ / sc, "us_per_step": ft / sc * 1e6,
                 "fwd_tflops": prof.select("coatt_flash_fwd")[1] / max(prof.select("coatt_flash_fwd")[2], 1e-12) / 1e12,
-                "bwd_tflops": prof.select("coatt_flash_bwd")[1] / max(prof.select("coatt_flash_bwd")[2], 1e-12) / 1e12}
+                "bwd_tflops": prof.select("coatt_flash_bwd")[1] / max(prof.select("coatt_flash_bwd")[2], 1e-12) / 1e12,
+                "algorithmic_gflop_per_step": ffl / sc / 1e9}
+            tr = coatt_trace()
+            if tr:
+                us = tr["train_us_per_step"]
+                out["roofline_coattention_train"]["rocprof"] = {
+                    "us_per_step": us, "frac": ffl / sc / (us * 1e-6) / 1e12 / peak, "source": tr["source"]}
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if prof and dtype == torch.bfloat16 and S == 473:
-        out["roofline_coattention"] = coattention_roofline(dev)
+        out["roofline_coattention"] = rc = coattention_roofline(dev)
+        tr = coatt_trace()
+        if tr and tr.get("configs3_us_per_launch"):
+            us = tr["configs3_us_per_launch"]
+            alg = rc["achieved"] * rc["us_per_launch"] * 1e-6 * 1e12
+            rc["rocprof"] = {"us_per_launch": us, "frac": alg / (us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                             "source": tr["source"]}
+    if args.fp32_extra and dtype == torch.bfloat16 and world == 1 and not args.no_roofline:
+        log("fp32 extra ...")
+        out["fp32_extra"] = fp32_extra(dev, B, S)
     out["build"] = __import__("cosnet_amd._native", fromlist=["build_info"]).build_info()
     if rank == 0 and args.cpu_baseline and world == 1:
         log("cpu baseline ...")
@@ -427,4 +493,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -17,7 +17,8 @@
 //   * P (<= 2^8 under the lazy rescale) quantised to e4m3 with unit scale; the row sum l is
 //     accumulated from the fp32 P.
 // A prepass (coatt_f8_rows_k, coatt_f8_vt_k) writes the MX images into a caller-owned workspace:
-//   rows:  X8 [B][HWp][256] bytes, Xs [B][HWp][8] (byte 4h + kk = block 2kk + h, the byte the
+//   rows:  X8 [B][HWp][256] bytes (HWp = ceil128(HW): whole query blocks), Xs [B][HWp][8]
+//          (byte 4h + kk = block 2kk + h, the byte the
 //          lane half h of MFMA step kk needs at opsel kk);
 //   V^T:   VT8 [B][nt][256][64] per 64-key tile, the keys of lane half h in the accumulator order
 //          key(h, j) = 32 (j >> 4) + (j & 3) + 8 ((j & 15) >> 2) + 4 h (so P needs no permute);
@@ -363,10 +364,13 @@ void coatt_f8_fwd_k(F8Args a) {
 }  // namespace
 
 static inline int hwp64(int HW) { return (HW + KT - 1) / KT * KT; }
+// row images hold whole 128-row query blocks (rows >= HW are zeros), so the last block's Q
+// loads stay inside its own batch entry's image
+static inline int hwq128(int HW) { return (HW + QB - 1) / QB * QB; }
 
 // workspace: two row images (Va_t, Vb) + two V^T images (Vb, Va), each with its scales
 extern "C" size_t cn_coatt_f8_workspace_bytes(int B, int HW) {
-  const size_t rows = (size_t)B * hwp64(HW);
+  const size_t rows = (size_t)B * hwq128(HW);
   const size_t nt = (size_t)hwp64(HW) / KT;
   return 2 * rows * (D + 8) + 2 * (size_t)B * nt * (VBYTES + 512) + 256;
 }
@@ -383,7 +387,7 @@ extern "C" int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va
       ((uintptr_t)zb & 7))
     return CN_ERR_ALIGN;
   if (!ws || ((uintptr_t)ws & 255) || ws_bytes < cn_coatt_f8_workspace_bytes(B, HW)) return CN_ERR_SHAPE;
-  const int HWp = hwp64(HW), nt = HWp / KT;
+  const int HWp = hwq128(HW), nt = hwp64(HW) / KT;
   const size_t rows = (size_t)B * HWp;
   unsigned char* p = (unsigned char*)ws;
   unsigned char* a8 = p;              p += rows * D;

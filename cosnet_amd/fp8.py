@@ -131,7 +131,8 @@ class Fp8Weights:
             self._table_ptrs = ptrs
         if capturing:
             self._captured = True
-            self._graph_tables.append(self._table)
+            if not any(t is self._table for t in self._graph_tables):
+                self._graph_tables.append(self._table)   # one reference per distinct table
         nv.call("cn_fp8_quant_multi", self._table.data_ptr(), self._table_n, nv.stream())
         for e in self._c.values():
             e[2] = self._tag(e[3]) if e[3] is not None else None

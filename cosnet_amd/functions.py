@@ -281,14 +281,13 @@ class CoattFn(F):
                 else:
                     ops.coatt_fused(vat, va, vb, n, hw, za, zb)                  # :160-170
                 return za, zb
-            # training: keep the per-row normalisers; the backward recomputes P from them (in
-            # bf16; with the fp8 forward the normalisers are the fp8 affinity's)
+            # training: keep the per-row normalisers; the backward recomputes P from them.  The
+            # training forward is the bf16 flash kernel in fp8 mode too, so the backward's
+            # recomputed S and P are exactly the ones the forward normalised (the MX-fp8
+            # affinity serves the no-grad path above)
             lse_a = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=dev)
             lse_b = torch.empty_like(lse_a)
-            if fp8:
-                ops.coatt_f8(vat, va, vb, n, hw, za, zb, lse_a, lse_b)          # :160-170
-            else:
-                ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)   # :160-170
+            ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)       # :160-170
             ctx.s = (va, vb, wf, vat, za, zb, lse_a, lse_b)
             ctx.flash = True
             ctx.link = link

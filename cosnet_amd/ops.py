@@ -518,7 +518,9 @@ def coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw, dva=
                     dva_accumulate=False):
     """Backward of the flash co-attention: returns dVa_t [P, C] (bf16) and, if `dva` is given,
     accumulates dV_a's softmax-over-i term sum_j P1[i][j] dZ_b[j] into it.  Algorithmic work
-    (the reference's autograd): 4 x 2 HW^2 C per pair with both gradients."""
+    (the reference's autograd; the recomputed S is not counted): dP0 = dZa Vb^T
+    and/or dP1 = Va dZb^T plus dVa_t = dS Vb in the dVa_t kernel, P1^T dZb in the PV kernel --
+    4 x 2 HW^2 C per pair with both gradients, 2 with dZa only."""
     c = vat.shape[1]
     P = n * hw
     hwp = hw_pad(hw)
@@ -534,7 +536,7 @@ def coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw, dva=
                 hwp, d1.data_ptr(), nv.stream())
     dvat = torch.empty((P, c), dtype=vat.dtype, device=dev)
     nterm = (dza is not None) + (dzb is not None)
-    ev = _prof_start((1 + 2 * nterm) * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
+    ev = _prof_start((1 + nterm) * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
                      (2 + 2 * nterm) * P * c * vat.element_size())
     # one workspace for the key-split partials of both kernels (they run one after the other)
     nws = max(int(nv.query("cn_coatt_flash_bwd_workspace_bytes", n, hw)),
@@ -546,7 +548,7 @@ def coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw, dva=
             nv.ptr(d1), n, hw, c, dvat.data_ptr(), ld(dvat), 0, nv.ptr(ws), nws, nv.stream())
     _prof_end(ev)
     if dva is not None and dzb is not None:
-        ev = _prof_start(2 * 2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
+        ev = _prof_start(2.0 * n * hw * hw * c, ("coatt_flash_bwd", n, hw, c),
                          3 * P * c * vat.element_size())
         nv.call("cn_coatt_flash_pv_ws", vat.data_ptr(), ld(vat), vb.data_ptr(), ld(vb), dzb.data_ptr(),
                 ld(dzb), lse_b.data_ptr(), n, hw, c, dva.data_ptr(), ld(dva), int(dva_accumulate),

@@ -117,6 +117,13 @@ def frame_resize(src, window, out_hw, mode, flip=False, mean=None, channels_last
     return out
 
 
+def augmented_hw(hh, ww, crop_ratio, scale_ratio):
+    """Crop then scale sizes of one training frame (utils.crop2d :32-46, int(ratio * size);
+    utils.scale2d :18-23): ((ch, cw), (sh, sw))."""
+    ch, cw = int(crop_ratio * hh), int(crop_ratio * ww)
+    return (ch, cw), (int(ch * scale_ratio), int(cw * scale_ratio))
+
+
 class SBMRGBD:
     """sbm_rgbd (dataloaders/sbm_rgbd_loader.py:201-722) returning GPU tensors.
 
@@ -241,12 +248,11 @@ class SBMRGBD:
         # utils.crop2d (:32-46): int(ratio * size), offset drawn once per frame (shared by rgb,
         # depth, gt of that frame)
         hh, ww = x.shape[1], x.shape[2]
-        ch, cw = int(self._crop_ratio * hh), int(self._crop_ratio * ww)
+        (ch, cw), (sh, sw) = augmented_hw(hh, ww, self._crop_ratio, self._scale_ratio)
         if offset is None:  # rows first, then columns (utils.py:36-37)
             oy = self.rng.choice(range(hh - ch))
             offset = {"x": self.rng.choice(range(ww - cw)), "y": oy}
         # utils.scale2d (:18-23) then flip2d (:5-9)
-        sh, sw = int(ch * self._scale_ratio), int(cw * self._scale_ratio)
         y = frame_resize(x, (offset["y"], offset["y"] + ch, offset["x"], offset["x"] + cw), (sh, sw),
                          mode, flip=self._flip_p(seq) > 0.5)
         return y, offset

@@ -431,34 +431,51 @@ class ShapeGraphCache:
         self.capacity, self.min_hits = capacity, min_hits
         self.graphs = OrderedDict()      # (h, w) -> TrainStep (recorded)
         self.seen = {}
+        self.evicted = set()             # sizes whose graph was evicted: never recorded again
         self.eager = None
         self.hits = self.records = self.eager_steps = 0
+
+    def admit(self, hw, batch):
+        """Policy for a batch of frame size `hw`: "hit" (replay its graph), "record" (record a
+        graph for it now; the LRU graph is evicted when full) or "eager".  A size is recorded
+        on its `min_hits`-th occurrence and at most once: an evicted size stays eager, so a
+        stream of non-recurring sizes cannot make every batch pay a capture (each costs an
+        eager step, a capture, an instantiation and a private memory pool)."""
+        if hw in self.graphs:
+            self.graphs.move_to_end(hw)
+            self.hits += 1
+            return "hit"
+        self.seen[hw] = self.seen.get(hw, 0) + 1
+        if (self.seen[hw] >= self.min_hits and self.capacity > 0 and batch == self.batch
+                and hw not in self.evicted):
+            if len(self.graphs) >= self.capacity:
+                old, _ = self.graphs.popitem(last=False)
+                self.evicted.add(old)
+            self.graphs[hw] = None
+            self.records += 1
+            return "record"
+        self.eager_steps += 1
+        return "eager"
 
     def __call__(self, rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b, lrs):
         hw = tuple(rgb_a.shape[2:])
         ins = (rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b)
-        st = self.graphs.get(hw)
-        if st is not None:
-            self.graphs.move_to_end(hw)
-            self.hits += 1
+        act = self.admit(hw, rgb_a.shape[0])
+        if act == "hit":
+            st = self.graphs[hw]
             st.load(*ins)
             return st(lrs)
-        self.seen[hw] = self.seen.get(hw, 0) + 1
-        if self.seen[hw] >= self.min_hits and self.capacity > 0 and rgb_a.shape[0] == self.batch:
-            if len(self.graphs) >= self.capacity:
-                self.graphs.popitem(last=False)
+        if act == "record":
             st = TrainStep(self.model, self.opt, self.batch, hw, l1_weight=self.l1, graphed=True,
                            grad_dtype=self.grad_dtype)
             st.load(*ins)
             self.opt.set_lrs(lrs)
             st.capture(warmup=1)          # this batch's step runs eagerly, then the record
             self.graphs[hw] = st
-            self.records += 1
             return st.loss
         if self.eager is None:
             self.eager = TrainStep(self.model, self.opt, self.batch, hw, l1_weight=self.l1,
                                    graphed=False, grad_dtype=self.grad_dtype)
-        self.eager_steps += 1
         return self.eager.run_batch(*ins, lrs)
 
     def sync_buffers(self, src=0):

@@ -85,3 +85,26 @@ def test_uninitialised_buffers_are_never_read(cuda, monkeypatch):
     for k in clean:
         assert torch.isfinite(clean[k]).all(), k
         assert torch.equal(clean[k], dirty[k]), (k, (clean[k] - dirty[k]).abs().max().item())
+
+
+def test_coatt_f8_workspace_tail_is_never_read(cuda, monkeypatch):
+    """The MX-fp8 co-attention's workspace (row images, V^T tiles, E8M0 scales) at HW = 3600,
+    where the 64-key padding (3648) leaves half a 128-row query block: the last block's Q rows and
+    scales must come from the zero-padded image of its own batch entry, never from whatever the
+    workspace holds next (0xA5 bytes = finite e4m3 values with 2^38 scales when poisoned)."""
+    n, hw, c = 2, 3600, 256
+    g = torch.Generator().manual_seed(9)
+    vat, va, vb = [(torch.randn((n * hw, c), generator=g) * 0.7).to(torch.bfloat16).to(cuda)
+                   for _ in range(3)]
+    res = []
+    for poison in (False, True):
+        monkeypatch.setattr(ops, "torch", _Alloc(torch, poison))
+        za = torch.zeros((n * hw, c), dtype=torch.bfloat16, device=cuda)
+        zb = torch.zeros_like(za)
+        la = torch.zeros((n, ops.hw_pad(hw)), dtype=torch.float32, device=cuda)
+        lb = torch.zeros_like(la)
+        ops.coatt_f8(vat, va, vb, n, hw, za, zb, la, lb)
+        torch.cuda.synchronize()
+        res.append([t.float().cpu() for t in (za, zb, la[:, :hw], lb[:, :hw])])
+    for a, b in zip(*res):
+        assert torch.isfinite(a).all() and torch.equal(a, b)

@@ -169,3 +169,33 @@ def test_train_and_test_cli_on_sbm_tree(cuda, tmp_path):
             for f in fs if f.endswith("_test_log.txt")]
     ious = [float(x) for x in re.findall(r"IOU: ([0-9.eE+-]+)==##", open(logs[0]).read())]
     assert len(ious) == 8 + 1 and all(0.0 <= v <= 1.0 for v in ious)
+
+
+def test_graph_cache_policy_on_loader_sizes():
+    """ShapeGraphCache's admission policy (no GPU: TrainStep is never built here) on the frame
+    sizes the loader produces (per-batch uniform scale 0.7-1.3 x crop 0.8-1, sbm_rgbd_loader.py:
+    700-702, output 473x473): ~340 distinct sizes, so 24 LRU slots hit on under 20 % of batches.
+    Sizes are recorded at most once (an evicted size stays eager), so the records are bounded by
+    the number of distinct sizes instead of growing with every batch; train.py leaves the cache
+    off by default."""
+    import random
+    from cosnet_amd.train_step import ShapeGraphCache
+    import train
+    assert train.get_arguments(["--dataset", "sbmrgbd"]).graph_cache == 0
+    rng = random.Random(0)
+    c = ShapeGraphCache(None, None, 4, capacity=24, min_hits=2)
+    seen = set()
+    n = 3000
+    for _ in range(n):
+        scale, crop = rng.uniform(0.7, 1.3), rng.uniform(0.8, 1)
+        _, hw = S.augmented_hw(473, 473, crop, scale)
+        seen.add(hw)
+        c.admit(hw, 4)
+    assert c.hits + c.records + c.eager_steps == n
+    assert c.hits / n < 0.2 and c.records <= len(seen), (c.hits, c.records, len(seen))
+    assert len(c.evicted) == c.records - len(c.graphs)
+    # a recurring size is recorded once and then replayed
+    c2 = ShapeGraphCache(None, None, 2, capacity=2, min_hits=2)
+    acts = [c2.admit(hw, 2) for hw in [(65, 81), (65, 81), (65, 81), (49, 65), (49, 65), (73, 57),
+                                       (73, 57), (65, 81), (65, 81)]]
+    assert acts == ["eager", "record", "hit", "eager", "record", "eager", "record", "eager", "eager"]
