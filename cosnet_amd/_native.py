@@ -95,6 +95,7 @@ _SIGS = {
     "cn_frame_resize": (_I, [_I, _P, _I, _L, _L, _L, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _P]),
     "cn_gemm_force_config": (_I, [_I]),
     "cn_gemm_set_wgrad_target": (_I, [_I]),
+    "cn_coatt_force_variant": (_I, [_I]),
     "cn_head_fwd": (_I, [_I, _P, _L, _P, _L, _I, _I, _I, _P, _P, _P, _L, _P, _P]),
     "cn_head_bwd": (_I, [_I, _P, _L, _P, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P]),
     "cn_upsample_sigmoid": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),

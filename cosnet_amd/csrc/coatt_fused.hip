@@ -24,6 +24,7 @@
 //     source address, so the DMA writes stay lane-linear.
 //   * O is rescaled only when some row's running max grew (wave-uniform branch, exact).
 #include "common.h"
+#include <cstdlib>
 #include "../../include/cosnet_hip.h"
 
 namespace {
@@ -417,6 +418,559 @@ void coatt_fused_fwd_k(FusedArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two waves per SIMD (coatt_fused2_k): the same flash product, 8 waves = 4 wave PAIRS per
+// workgroup, 128 query rows.  Both waves of a pair hold the pair's 32 query rows in registers (Q,
+// 64 VGPRs) and compute the same S^T tile and softmax (identical instruction streams: identical
+// bits), and each accumulates ONE half of the output channels (O^T for d in [128 hb, +128): 64
+// accumulators instead of 128).  So a wave fits in 256 registers and every SIMD runs two of them:
+// one wave's MFMAs overlap the other's softmax, LDS waits and LDS-DMA issue, which the 4-wave
+// kernel (one wave per SIMD) serialises.  The price is the duplicated S product (1.5x the MFMAs
+// of the algorithmic count).  Waves 4-7 run half a tile (one phase) behind waves 0-3 (guide: two
+// waves of one program per SIMD, stagger): phase 1 = S + softmax, phase 2 = PV + refill, one
+// barrier each; the K/V ring is 4 stages deep so the lagging half still reads its tile while the
+// leading half refills two tiles ahead.
+constexpr int F2STAGES = 4;
+constexpr int F2NT = 512;
+constexpr int F2NP = 2 * FTILE / (16 * F2NT);    // LDS-DMA instructions per thread per K/V tile (4)
+
+template <int MODE>
+__global__ __launch_bounds__(F2NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void coatt_fused2_k(FusedArgs a) {
+  // [stage s: K 16 KB | V 16 KB] x 4, then (MODE 1) the per-key normalisers of each stage's tile
+  __shared__ __attribute__((aligned(16))) char lds[F2STAGES * 2 * FTILE + F2STAGES * FBK * 4];
+  constexpr int NP = F2NP + (MODE == 1);        // LDS-DMA instructions per thread per tile
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int grp = w >> 2;                       // stagger group (waves 4-7 lag one phase)
+  const int pair = (w >> 1) & 1 ? 2 * grp + 1 : 2 * grp;
+  const int hb = w & 1;                         // output-channel half of this wave
+  const int nfull8 = (a.nfull + 7) & ~7;
+  int item, split = 0;
+  bool live = true;
+  if ((int)blockIdx.x < nfull8) {
+    const int per_xcd = nfull8 >> 3;
+    item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    live = item < a.nfull;
+  } else {
+    const int t = blockIdx.x - nfull8;
+    item = a.nfull + t / a.nsplit;
+    split = t % a.nsplit;
+    live = item < a.nitems;
+  }
+  if (!live) return;                            // whole workgroup: uniform
+  const bool part = item >= a.nfull;
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const int HW = a.HW;
+  const long long b = bd / a.ndir;
+  const bf16* Q = d.q + b * HW * d.ldq;
+  const bf16* K = d.k + b * HW * d.ldk;
+  const bf16* V = d.v + b * HW * d.ldv;
+  const int q0 = rb * FBQ;
+  const int qrow = q0 + pair * 32 + r;
+  const bool qok = qrow < HW;
+  const void* zp = (const void*)g_zero16_fused;
+  const float L2E = 1.4426950408889634f;
+
+  // the pair's query rows as B fragments of S^T = K Q^T (k-step ks: d = 16 ks + 8 h .. +7)
+  bf16x8 qreg[16];
+  {
+    const bf16* src = Q + (long long)(qok ? qrow : 0) * d.ldq + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) qreg[ks] = qok ? *(const bf16x8*)(src + 16 * ks) : bf16x8{};
+  }
+
+  const int ntiles = (HW + FBK - 1) / FBK;
+  const int tb = part ? split * a.tps : 0;
+  const int nt = part ? min(ntiles - tb, a.tps) : ntiles;
+  // piece i (< 2) of tile t's K and V images: chunk p = 512 i + tid -> key row p >> 5, position
+  // p & 31 (the 4-wave kernel's images: K chunk ^ (row & 15), V chunk ^ ((row & 3) << 2))
+  auto issue_piece = [&](int t, int i) {
+    char* kb = lds + ((t & (F2STAGES - 1)) * 2) * FTILE;
+    char* vb = kb + FTILE;
+    const int p = i * F2NT + tid;
+    const int row = p >> 5, cpos = p & 31;
+    const int key = (tb + t) * FBK + row;
+    const bool ok = key < HW;
+    const bf16* ks = K + (long long)key * d.ldk + ((cpos ^ (row & 15)) << 3);
+    const bf16* vs = V + (long long)key * d.ldv + ((cpos ^ ((row & 3) << 2)) << 3);
+    const int wb = (i * F2NT + (tid & ~63)) * 16;
+    glds16f(ok ? (const void*)ks : zp, kb + wb);
+    glds16f(ok ? (const void*)vs : zp, vb + wb);
+  };
+  // MODE 1: the tile's 32 per-key normalisers (128 B, +inf padded to HWp) by lanes 0-7 of every
+  // wave (same bytes to the same place), so each wave's DMA count per tile stays uniform
+  auto issue_klse = [&](int t) {
+    if constexpr (MODE == 1) {
+      char* kl = lds + F2STAGES * 2 * FTILE + (t & (F2STAGES - 1)) * FBK * 4;
+      if (lane < 8) glds16f(d.klse + b * a.HWp + (tb + t) * FBK + 4 * lane, kl);
+    }
+  };
+  // prologue: tiles 0..2 in flight, tile 0 landed
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (t < nt) { issue_piece(t, 0); issue_piece(t, 1); issue_klse(t); }
+  // vmcnt: the Q loads are older than every DMA piece, so counted waits cover them too
+  if (nt >= 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NP) : "memory");
+  else if (nt == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier_f();
+  if (grp) raw_barrier_f();                     // the stagger: waves 4-7 one phase behind
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, l = 0.f;
+  const int sw = r & 15;
+  const int G = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+
+  for (int t = 0; t < nt; ++t) {
+    const char* kb = lds + ((t & (F2STAGES - 1)) * 2) * FTILE;
+    const char* vb = kb + FTILE;
+    f32x4 nk[4];
+    if constexpr (MODE == 1) {   // lane's keys 32t + 8q + 4h + 0..3
+      const float* kl = (const float*)(lds + F2STAGES * 2 * FTILE + (t & (F2STAGES - 1)) * FBK * 4) + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nk[q] = *(const f32x4*)(kl + 8 * q);
+    }
+    // ---- phase 1: S^T = K Q^T (32 keys x the pair's 32 queries), softmax -> P
+    f32x16 s = f32x16{};
+    {
+      constexpr int KPF = 3;
+      const char* krp = kb + r * FROWB;
+      bf16x8 kf[KPF];
+#pragma unroll
+      for (int u = 0; u < KPF; ++u) kf[u] = *(const bf16x8*)(krp + (((2 * u + h) ^ sw) << 4));
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        const bf16x8 kc = kf[ks % KPF];
+        if (ks + KPF < 16) kf[ks % KPF] = *(const bf16x8*)(krp + (((2 * (ks + KPF) + h) ^ sw) << 4));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kc, qreg[ks], s, 0, 0, 0);
+      }
+    }
+    bf16x8 pf[2];
+    const int key0 = (tb + t) * FBK;
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = 8 * s2 + j;
+          pv[j] = __builtin_amdgcn_exp2f(fmaf(s[i], L2E, -nk[i >> 2][i & 3]));
+        }
+        pf[s2] = pack8(pv);
+      }
+    } else {
+      if (key0 + FBK > HW) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (key0 + (i & 3) + 8 * (i >> 2) + 4 * h >= HW) s[i] = -INFINITY;
+      }
+      float mx = s[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, s[i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx * L2E);
+      if (__builtin_amdgcn_ballot_w64(mnew > m + RESCALE_T) != 0) {
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        m = mnew;
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pv[j] = __builtin_amdgcn_exp2f(fmaf(s[8 * s2 + j], L2E, -m));
+          l += pv[j];
+        }
+        pf[s2] = pack8(pv);
+      }
+    }
+    // end of phase 1: tile t+1 landed (this wave's pieces; tile t+2's may stay in flight)
+    if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_f();
+
+    // ---- phase 2: O^T[this half] += V^T P^T over the tile's 32 keys; refill tile t+3
+    const bool dodma = t + 3 < nt;
+    {
+      const unsigned vrow = lds_addr(vb + (4 * h + q4) * FROWB);
+      auto vread = [&](int dt, int sk) {
+        const int g = 8 * (4 * hb + dt) + 4 * (G & 1) + pp;
+        const unsigned a1 = vrow + 16 * sk * FROWB + ((g ^ (q4 << 3)) << 3);
+        u32x2 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a1));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "n"(8 * FROWB));
+        u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+        return __builtin_bit_cast(bf16x8, v);
+      };
+      constexpr int VPF = 3;
+      bf16x8 vf[VPF];
+#pragma unroll
+      for (int u = 0; u < VPF; ++u) vf[u] = vread(u >> 1, u & 1);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        bf16x8 cur = vf[it % VPF];
+        if (it + VPF < 8) vf[it % VPF] = vread((it + VPF) >> 1, (it + VPF) & 1);
+        const int younger = 2 * (7 - it < VPF ? 7 - it : VPF);
+        if (younger >= 6) lgkm_wait<6>(cur);
+        else if (younger == 4) lgkm_wait<4>(cur);
+        else if (younger == 2) lgkm_wait<2>(cur);
+        else lgkm_wait<0>(cur);
+        o[it >> 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, pf[it & 1], o[it >> 1], 0, 0, 0);
+        if ((it & 3) == 1 && dodma) issue_piece(t + 3, it >> 2);
+      }
+      if (dodma) issue_klse(t + 3);
+    }
+    // end of phase 2: tile t+1 landed (tiles t+2, t+3 may stay in flight)
+    if (t + 3 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NP) : "memory");
+    else if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_f();
+  }
+  if (!grp) raw_barrier_f();                    // equal barrier counts for both halves
+
+  // ---- epilogue: this wave's half of O; register i of tile dt: d = 128 hb + 32 dt + (i&3) + 8(i>>2) + 4h
+  l += __shfl_xor(l, 32, 64);
+  if (part) {
+    if (qok) {
+      const long long prow = ((long long)split * (a.nitems - a.nfull) + (item - a.nfull)) * FBQ + (qrow - q0);
+      float* op = a.opart + prow * FD + 128 * hb + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          *(f32x4*)(op + 32 * dt + 8 * c) = f32x4{o[dt][4 * c], o[dt][4 * c + 1], o[dt][4 * c + 2], o[dt][4 * c + 3]};
+      if (MODE == 0 && h == 0 && hb == 0) *(float2*)(a.mlpart + prow * 2) = float2{m, l};
+    }
+    return;
+  }
+  if (MODE == 0 && d.lse && h == 0 && hb == 0 && qrow < a.HWp)
+    d.lse[b * a.HWp + qrow] = qok ? m + __builtin_amdgcn_logf(l) : INFINITY;
+  if (qok) {
+    const float inv = MODE == 0 ? 1.f / l : 1.f;
+    bf16* op = d.o + (b * HW + qrow) * d.ldo + 128 * hb + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 v;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + 32 * dt + 8 * c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv + (float)old[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+        }
+        *(bf16x4*)(op + 32 * dt + 8 * c) = v;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave pairs WITHOUT the duplicated S product (coatt_fused3_k): both waves of a pair hold the
+// pair's 32 query rows (Q, 64 VGPRs) but split each 32-key tile -- wave hb computes S^T for keys
+// [16 hb, +16) on v_mfma_f32_16x16x32_bf16 (8 values per lane: 4 keys x 2 queries) -- and the
+// output channels [128 hb, +128) of O.  Per tile the pair exchanges through LDS its partial row
+// maxima (128 B per wave) and its half of P (bf16, 1 KB per wave, [query][key] with a 16-B
+// chunk XOR (q >> 2) & 3), so each wave runs the PV product over all 32 keys for its channels.
+// Three phases per tile, one barrier each: [S + partial max] [pair max, rescale, P] [PV + refill];
+// waves 4-7 lag one phase.  The row sums stay per wave (own keys) and are added once at the end.
+// Algorithmic MFMA count (no duplicated S); S is summed in a different order than the 4-wave
+// kernel's 32x32x16 product (not bitwise equal to it).
+constexpr int F3PB = 32 * 32 * 2;        // P of one pair: [32 queries][32 keys] bf16
+
+template <int MODE>
+__global__ __launch_bounds__(F2NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void coatt_fused3_k(FusedArgs a) {
+  constexpr int RING = F2STAGES * 2 * FTILE;
+  constexpr int KLB = F2STAGES * FBK * 4;
+  // [K/V ring 128 KB][klse ring][P of 4 pairs 8 KB][row max / sum exchange: 8 waves x 32 floats]
+  __shared__ __attribute__((aligned(16))) char lds[RING + KLB + 4 * F3PB + 8 * 32 * 4];
+  constexpr int NP = F2NP + (MODE == 1);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;            // O layout (32x32 accumulators)
+  const int c16 = lane & 15, g4 = lane >> 4;         // S layout (16x16 accumulators)
+  const int grp = w >> 2;
+  const int pair = (w >> 1) & 1 ? 2 * grp + 1 : 2 * grp;
+  const int hb = w & 1;
+  const int nfull8 = (a.nfull + 7) & ~7;
+  int item, split = 0;
+  bool live = true;
+  if ((int)blockIdx.x < nfull8) {
+    const int per_xcd = nfull8 >> 3;
+    item = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    live = item < a.nfull;
+  } else {
+    const int t = blockIdx.x - nfull8;
+    item = a.nfull + t / a.nsplit;
+    split = t % a.nsplit;
+    live = item < a.nitems;
+  }
+  if (!live) return;
+  const bool part = item >= a.nfull;
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const int HW = a.HW;
+  const long long b = bd / a.ndir;
+  const bf16* Q = d.q + b * HW * d.ldq;
+  const bf16* K = d.k + b * HW * d.ldk;
+  const bf16* V = d.v + b * HW * d.ldv;
+  const int q0 = rb * FBQ;
+  const int qrow = q0 + pair * 32 + r;
+  const bool qok = qrow < HW;
+  const void* zp = (const void*)g_zero16_fused;
+  const float L2E = 1.4426950408889634f;
+  char* pbuf = lds + RING + KLB + pair * F3PB;
+  float* xch = (float*)(lds + RING + KLB + 4 * F3PB);       // [8][32]
+  float* xmine = xch + w * 32;
+  const float* xpart = xch + (w ^ 1) * 32;
+
+  // Q as B fragments of S^T = K Q^T (16x16x32): q-block qb, d chunk ks -> query 16 qb + c16,
+  // d = 32 ks + 8 g4 + 0..7
+  bf16x8 qreg[2][8];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int row = q0 + pair * 32 + 16 * qb + c16;
+    const bool ok = row < HW;
+    const bf16* src = Q + (long long)(ok ? row : 0) * d.ldq + 8 * g4;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qreg[qb][ks] = ok ? *(const bf16x8*)(src + 32 * ks) : bf16x8{};
+  }
+
+  const int ntiles = (HW + FBK - 1) / FBK;
+  const int tb = part ? split * a.tps : 0;
+  const int nt = part ? min(ntiles - tb, a.tps) : ntiles;
+  auto issue_piece = [&](int t, int i) {
+    char* kb = lds + ((t & (F2STAGES - 1)) * 2) * FTILE;
+    char* vb = kb + FTILE;
+    const int p = i * F2NT + tid;
+    const int row = p >> 5, cpos = p & 31;
+    const int key = (tb + t) * FBK + row;
+    const bool ok = key < HW;
+    const bf16* ks = K + (long long)key * d.ldk + ((cpos ^ (row & 15)) << 3);
+    const bf16* vs = V + (long long)key * d.ldv + ((cpos ^ ((row & 3) << 2)) << 3);
+    const int wb = (i * F2NT + (tid & ~63)) * 16;
+    glds16f(ok ? (const void*)ks : zp, kb + wb);
+    glds16f(ok ? (const void*)vs : zp, vb + wb);
+  };
+  auto issue_klse = [&](int t) {
+    if constexpr (MODE == 1) {
+      char* kl = lds + RING + (t & (F2STAGES - 1)) * FBK * 4;
+      if (lane < 8) glds16f(d.klse + b * a.HWp + (tb + t) * FBK + 4 * lane, kl);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (t < nt) { issue_piece(t, 0); issue_piece(t, 1); issue_klse(t); }
+  if (nt >= 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NP) : "memory");
+  else if (nt == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier_f();
+  if (grp) raw_barrier_f();
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+  float ms[2] = {-INFINITY, -INFINITY}, ls[2] = {0.f, 0.f};   // S layout: queries 16 qb + c16
+  float mo = -INFINITY;                                       // O layout: query r
+  const int G = lane >> 4, q4 = (lane & 15) >> 2, pp = lane & 3;
+  const int krow = 16 * hb + c16;                             // this lane's key row of the tile
+
+  auto wait_t1 = [&](int t, bool after_refill) {   // tile t+1 landed (this wave's pieces)
+    if (after_refill && t + 3 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NP) : "memory");
+    else if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  for (int t = 0; t < nt; ++t) {
+    const char* kb = lds + ((t & (F2STAGES - 1)) * 2) * FTILE;
+    const char* vb = kb + FTILE;
+    const int key0 = (tb + t) * FBK;
+    // ---- phase A: S^T for this wave's 16 keys x the pair's 32 queries; partial row max
+    f32x4 s[2] = {f32x4{}, f32x4{}};
+    {
+      constexpr int KPF = 3;
+      const char* kr = kb + krow * FROWB;
+      bf16x8 kf[KPF];
+#pragma unroll
+      for (int u = 0; u < KPF; ++u) kf[u] = *(const bf16x8*)(kr + (((4 * u + g4) ^ c16) << 4));
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 kc = kf[ks % KPF];
+        if (ks + KPF < 8) kf[ks % KPF] = *(const bf16x8*)(kr + (((4 * (ks + KPF) + g4) ^ c16) << 4));
+        s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kc, qreg[0][ks], s[0], 0, 0, 0);
+        s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kc, qreg[1][ks], s[1], 0, 0, 0);
+      }
+    }
+    // register i of s[qb]: key key0 + 16 hb + 4 g4 + i, query 16 qb + c16
+    if constexpr (MODE == 0) {
+      if (key0 + FBK > HW) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (key0 + 16 * hb + 4 * g4 + i >= HW) s[qb][i] = -INFINITY;
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mx = fmaxf(fmaxf(s[qb][0], s[qb][1]), fmaxf(s[qb][2], s[qb][3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        if (g4 == 0) xmine[16 * qb + c16] = mx;
+      }
+    }
+    wait_t1(t, false);
+    raw_barrier_f();
+
+    // ---- phase B: pair row max, lazy rescale, P of this wave's keys -> the pair's P buffer
+    float pv[2][4];
+    if constexpr (MODE == 1) {
+      const f32x4 nk = *(const f32x4*)(lds + RING + (t & (F2STAGES - 1)) * FBK * 4 + (16 * hb + 4 * g4) * 4);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pv[qb][i] = __builtin_amdgcn_exp2f(fmaf(s[qb][i], L2E, -nk[i]));
+    } else {
+      float mn[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        mn[qb] = fmaxf(ms[qb], fmaxf(xmine[16 * qb + c16], xpart[16 * qb + c16]) * L2E);
+      const float mno = fmaxf(mo, fmaxf(xmine[r], xpart[r]) * L2E);
+      if (__builtin_amdgcn_ballot_w64(mn[0] > ms[0] + RESCALE_T || mn[1] > ms[1] + RESCALE_T) != 0) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          ls[qb] *= __builtin_amdgcn_exp2f(ms[qb] - mn[qb]);
+          ms[qb] = mn[qb];
+        }
+        const float alpha = __builtin_amdgcn_exp2f(mo - mno);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        mo = mno;
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pv[qb][i] = __builtin_amdgcn_exp2f(fmaf(s[qb][i], L2E, -ms[qb]));
+          ls[qb] += pv[qb][i];
+        }
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+      bf16x4 v4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v4[i] = (bf16)pv[qb][i];
+      const int q = 16 * qb + c16;
+      const int chunk = (2 * hb + (g4 >> 1)) ^ ((q >> 2) & 3);
+      *(bf16x4*)(pbuf + q * 64 + (chunk << 4) + 8 * (g4 & 1)) = v4;
+    }
+    wait_t1(t, false);
+    raw_barrier_f();
+
+    // ---- phase C: O^T[this half] += V^T P^T over all 32 keys; refill tile t+3
+    bf16x8 pf[2];
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk)
+      pf[sk] = *(const bf16x8*)(pbuf + r * 64 + (((2 * sk + h) ^ ((r >> 2) & 3)) << 4));
+    const bool dodma = t + 3 < nt;
+    {
+      const unsigned vrow = lds_addr(vb + (4 * h + q4) * FROWB);
+      auto vread = [&](int dt, int sk) {
+        const int g = 8 * (4 * hb + dt) + 4 * (G & 1) + pp;
+        const unsigned a1 = vrow + 16 * sk * FROWB + ((g ^ (q4 << 3)) << 3);
+        u32x2 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a1));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a1), "n"(8 * FROWB));
+        u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+        return __builtin_bit_cast(bf16x8, v);
+      };
+      constexpr int VPF = 3;
+      bf16x8 vf[VPF];
+#pragma unroll
+      for (int u = 0; u < VPF; ++u) vf[u] = vread(u >> 1, u & 1);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        bf16x8 cur = vf[it % VPF];
+        if (it + VPF < 8) vf[it % VPF] = vread((it + VPF) >> 1, (it + VPF) & 1);
+        const int younger = 2 * (7 - it < VPF ? 7 - it : VPF);
+        if (younger >= 6) lgkm_wait<6>(cur);
+        else if (younger == 4) lgkm_wait<4>(cur);
+        else if (younger == 2) lgkm_wait<2>(cur);
+        else lgkm_wait<0>(cur);
+        o[it >> 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, pf[it & 1], o[it >> 1], 0, 0, 0);
+        if ((it & 3) == 1 && dodma) issue_piece(t + 3, it >> 2);
+      }
+      if (dodma) issue_klse(t + 3);
+    }
+    wait_t1(t, true);
+    raw_barrier_f();
+  }
+  if (!grp) raw_barrier_f();
+
+  // ---- row sums: this wave's keys (S layout) -> per query, + the partner's (O layout)
+  float lo = 0.f;
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float v = ls[qb];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g4 == 0) xmine[16 * qb + c16] = v;
+    }
+    raw_barrier_f();
+    lo = xmine[r] + xpart[r];
+  }
+
+  if (part) {
+    if (qok) {
+      const long long prow = ((long long)split * (a.nitems - a.nfull) + (item - a.nfull)) * FBQ + (qrow - q0);
+      float* op = a.opart + prow * FD + 128 * hb + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          *(f32x4*)(op + 32 * dt + 8 * c) = f32x4{o[dt][4 * c], o[dt][4 * c + 1], o[dt][4 * c + 2], o[dt][4 * c + 3]};
+      if (MODE == 0 && h == 0 && hb == 0) *(float2*)(a.mlpart + prow * 2) = float2{mo, lo};
+    }
+    return;
+  }
+  if (MODE == 0 && d.lse && h == 0 && hb == 0 && qrow < a.HWp)
+    d.lse[b * a.HWp + qrow] = qok ? mo + __builtin_amdgcn_logf(lo) : INFINITY;
+  if (qok) {
+    const float inv = MODE == 0 ? 1.f / lo : 1.f;
+    bf16* op = d.o + (b * HW + qrow) * d.ldo + 128 * hb + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 v;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + 32 * dt + 8 * c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv + (float)old[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][4 * c + j] * inv);
+        }
+        *(bf16x4*)(op + 32 * dt + 8 * c) = v;
+      }
+  }
+}
+
 // Fold the key-split partials of one row of a tail item: O = sum_s 2^(m_s - M) O_s /
 // sum_s 2^(m_s - M) l_s, splits in order (deterministic).  One thread = 8 channels of one row.
 // MODE 1 (per-key normaliser, linear in the keys): O (+)= sum_s O_s.
@@ -495,6 +1049,27 @@ static void plan_split(int items, int ntiles, int* nfull, int* nsplit) {
   *nsplit = s;
 }
 
+// Kernel variant: 1 = coatt_fused_fwd_k (4 waves, one per SIMD), 2 = coatt_fused2_k (wave pairs,
+// duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys).  CN_COATT_VARIANT picks the
+// default; cn_coatt_force_variant overrides it (tests, A/B tools).
+static int g_coatt_variant = 0;
+static int coatt_variant() {
+  static const int v = [] {
+    const char* e = getenv("CN_COATT_VARIANT");
+    const int x = e ? atoi(e) : 1;
+    return (x >= 1 && x <= 3) ? x : 1;
+  }();
+  return g_coatt_variant ? g_coatt_variant : v;
+}
+
+// Development / test hook: force the forward / PV kernel variant (1, 2, 3 as above; 0: default).
+// Returns the previous setting.
+extern "C" int cn_coatt_force_variant(int v) {
+  const int old = g_coatt_variant;
+  g_coatt_variant = (v >= 1 && v <= 3) ? v : 0;
+  return old;
+}
+
 static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   a.ndir = nd;
   a.nrb = (a.HW + FBQ - 1) / FBQ;
@@ -505,8 +1080,17 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   const int nfull8 = (a.nfull + 7) & ~7;
   a.nwork = nfull8 + (a.nitems - a.nfull) * a.nsplit;
   dim3 grid(a.nwork);
-  if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
+  const int var = coatt_variant();
+  if (var == 2) {
+    if (mode == 0) hipLaunchKernelGGL(coatt_fused2_k<0>, grid, dim3(F2NT), 0, st, a);
+    else hipLaunchKernelGGL(coatt_fused2_k<1>, grid, dim3(F2NT), 0, st, a);
+  } else if (var == 3) {
+    if (mode == 0) hipLaunchKernelGGL(coatt_fused3_k<0>, grid, dim3(F2NT), 0, st, a);
+    else hipLaunchKernelGGL(coatt_fused3_k<1>, grid, dim3(F2NT), 0, st, a);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
+  }
   CN_CHECK_LAUNCH();
   if (a.nsplit > 1) {
     const long long threads = (long long)(a.nitems - a.nfull) * FBQ * (FD / 8);

@@ -12,6 +12,8 @@ reference differentiates.
 Reference blocks: stem deeplab/residual_net.py:157-160, Bottleneck :74-96, ASPP
 deeplab/deeplabv3_encoder.py:50-86.
 """
+import os
+
 import torch
 
 from . import _native as nv
@@ -45,6 +47,19 @@ class GradSink(dict):
                 dst.as_strided(p.shape, p.stride()).copy_(g)
             return
         super().__setitem__(p, g)
+
+
+# When the queued bottleneck weight gradients are issued in a single-process encoder backward:
+# "end" (after the whole dgrad chain) or "layer" (after each layer's blocks: the queue's dY and
+# input tensors are released per layer).  CN_WGRAD_FLUSH selects it for A/B runs.
+WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
+
+
+def _layer_index(enc):
+    """id(block) -> index of its ResNet layer."""
+    bb = enc.backbone
+    return {id(blk): i for i, layer in enumerate((bb.layer1, bb.layer2, bb.layer3, bb.layer4))
+            for blk in layer}
 
 
 class WgradQueue:
@@ -469,10 +484,20 @@ class EncoderPairFn(F):
         if f8 is not None:
             f8.grads.begin()
         wq = WgradQueue()
-        dx = aspp_bwd(rec[-1], dfa, grads)
-        for item in reversed(rec[1:-1]):
+        dx = aspp_bwd(rec.pop(), dfa, grads)
+        stem = rec[0]
+        blocks = rec[1:]
+        del rec[:]                         # each block's saved tensors die with its backward
+        layer_of = _layer_index(ctx.enc)
+        while blocks:
+            item = blocks.pop()
             dx = bottleneck_bwd(item, dx, grads, wq=wq)
-        stem_bwd(rec[0], dx, grads)
+            # WGRAD_FLUSH "layer": issue the queued weight gradients after the last (first in
+            # backward order) block of each layer, releasing their dY / input tensors there
+            if WGRAD_FLUSH == "layer" and (not blocks or layer_of[id(blocks[-1][1])] != layer_of[id(item[1])]):
+                wq.flush()
+            del item
+        stem_bwd(stem, dx, grads)
         wq.flush()
         if f8 is not None:
             f8.grads.end()   # advance the gradient scales from this backward's amax

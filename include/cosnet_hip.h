@@ -376,6 +376,10 @@ const char* cn_build_source_hash(void);
 int cn_gemm_force_config(int cfg);
 /* Development hook (tuning tools only): number of blocks the wgrad K split aims for. */
 int cn_gemm_set_wgrad_target(int blocks);
+/* Development / test hook: co-attention flash forward and PV kernel variant (1: four waves, one
+ * per SIMD; 2: eight waves in pairs that split the output channels, S computed by both; 3: pairs
+ * that split the keys of S and the output channels; 0: default).  Returns the previous setting. */
+int cn_coatt_force_variant(int v);
 
 #ifdef __cplusplus
 }

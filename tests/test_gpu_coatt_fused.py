@@ -160,3 +160,81 @@ def test_flash_training_fwd_bwd_vs_fp64(cuda, n, hw, which):
                            ("dW", Wg.grad, wr.grad)):
         e = rel(got, ref.detach())
         assert e <= 3e-2, (name, e)
+
+
+@pytest.mark.parametrize("n,hw", [(1, 97), (2, 169), (1, 1271), (4, 3600), (5, 3600)])
+def test_paired_wave_kernel_is_bitwise_the_four_wave_kernel(cuda, n, hw):
+    """The 8-wave forward (coatt_fused2_k: wave pairs share 32 query rows and split the output
+    channels, two waves per SIMD) runs each S element, softmax step and P.V sum with the same
+    MFMA sequence as the 4-wave kernel: no-grad forward (incl. the key-split tail), training
+    forward (LSE) and the PV backward kernel (per-key normaliser, accumulate) are bitwise equal."""
+    lib = nv.load()
+    vat, va, vb = make(n, hw, 256, cuda, seed=hw + 7, scale=0.8)
+    g = torch.Generator().manual_seed(n * hw)
+    dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    old = lib.cn_coatt_force_variant(1)
+    try:
+        for v in (1, 2):
+            lib.cn_coatt_force_variant(v)
+            za, zb = ops.coatt_fused(vat, va, vb, n, hw, torch.empty_like(va), torch.empty_like(va))
+            la = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=cuda)
+            lb = torch.empty_like(la)
+            ta, tb = torch.empty_like(va), torch.empty_like(va)
+            ops.coatt_flash_fwd(vat, va, vb, n, hw, ta, tb, la, lb)
+            pv = (torch.randn((n * hw, 256), generator=torch.Generator().manual_seed(3)) * 0.1) \
+                .to(torch.bfloat16).to(cuda)
+            nws = int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, 1))
+            ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=cuda)
+            nv.call("cn_coatt_flash_pv_ws", vat.data_ptr(), ops.ld(vat), vb.data_ptr(), ops.ld(vb),
+                    dzb.data_ptr(), ops.ld(dzb), lb.data_ptr(), n, hw, 256, pv.data_ptr(), ops.ld(pv),
+                    1, ws.data_ptr(), nws, nv.stream())
+            torch.cuda.synchronize()
+            outs.append([za, zb, ta, tb, la[:, :hw], lb[:, :hw], pv])
+    finally:
+        lib.cn_coatt_force_variant(old)
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert torch.isfinite(x.float()).all(), k
+        assert torch.equal(x, y), (k, (x.float() - y.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("n,hw", [(1, 1), (2, 63), (1, 97), (2, 169), (1, 1271), (4, 3600), (5, 3600)])
+def test_key_split_pair_kernel(cuda, n, hw):
+    """The 8-wave forward whose wave pairs split the keys of S (coatt_fused3_k, 16x16x32 S
+    products, pair-wise max / P exchange through LDS) against fp64 of rgbd_segmentation_RAA.py:
+    160-170 (no-grad forward incl. the key-split tail), and against the 4-wave kernel: training
+    forward's LSE to 1e-4 (only S's summation order differs) and the PV backward kernel within
+    the bf16 output rounding."""
+    lib = nv.load()
+    vat, va, vb = make(n, hw, 256, cuda, seed=hw + 11, scale=0.8)
+    g = torch.Generator().manual_seed(n * hw + 1)
+    dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    old = lib.cn_coatt_force_variant(1)
+    try:
+        for v in (1, 3):
+            lib.cn_coatt_force_variant(v)
+            za, zb = ops.coatt_fused(vat, va, vb, n, hw, torch.empty_like(va), torch.empty_like(va))
+            la = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=cuda)
+            lb = torch.empty_like(la)
+            ta, tb = torch.empty_like(va), torch.empty_like(va)
+            ops.coatt_flash_fwd(vat, va, vb, n, hw, ta, tb, la, lb)
+            pv = torch.zeros_like(va)
+            nws = int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, 1))
+            ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=cuda)
+            nv.call("cn_coatt_flash_pv_ws", vat.data_ptr(), ops.ld(vat), vb.data_ptr(), ops.ld(vb),
+                    dzb.data_ptr(), ops.ld(dzb), lb.data_ptr(), n, hw, 256, pv.data_ptr(), ops.ld(pv),
+                    0, ws.data_ptr(), nws, nv.stream())
+            torch.cuda.synchronize()
+            outs.append([za, zb, ta, tb, la[:, :hw], lb[:, :hw], pv])
+    finally:
+        lib.cn_coatt_force_variant(old)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    v3 = outs[1]
+    for got, ref in ((v3[0], ra), (v3[1], rb), (v3[2], ra), (v3[3], rb)):
+        assert torch.isfinite(got.float()).all()
+        assert rel(got, ref) <= TOL, rel(got, ref)
+    for k in (4, 5):
+        assert (outs[0][k] - v3[k]).abs().max().item() <= 1e-4 * max(1.0, outs[0][k].abs().max().item())
+    e = rel(v3[6], outs[0][6].double())
+    assert torch.isfinite(v3[6].float()).all() and e <= 8e-3, e
