@@ -681,8 +681,9 @@ void coatt_fused2_k(FusedArgs a) {
 // pair's 32 query rows (Q, 64 VGPRs) but split each 32-key tile -- wave hb computes S^T for keys
 // [16 hb, +16) on v_mfma_f32_16x16x32_bf16 (8 values per lane: 4 keys x 2 queries) -- and the
 // output channels [128 hb, +128) of O.  Per tile the pair exchanges through LDS its partial row
-// maxima (128 B per wave) and its half of P (bf16, 1 KB per wave, [query][key] with a 16-B
-// chunk XOR (q >> 2) & 3), so each wave runs the PV product over all 32 keys for its channels.
+// maxima (128 B per wave) and its half of P (bf16, 1 KB per wave, [query][32 keys in the PV
+// operand's k order] with a 16-B chunk XOR (q >> 2) & 3), so each wave runs the PV product over
+// all 32 keys for its channels.
 // Three phases per tile, one barrier each: [S + partial max] [pair max, rescale, P] [PV + refill];
 // waves 4-7 lag one phase.  The row sums stay per wave (own keys) and are added once at the end.
 // Algorithmic MFMA count (no duplicated S); S is summed in a different order than the 4-wave
@@ -830,6 +831,9 @@ void coatt_fused3_k(FusedArgs a) {
       }
     }
     wait_t1(t, false);
+    // the partner reads these LDS words after the barrier: the stores must have completed
+    // (s_barrier does not wait for them)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier_f();
 
     // ---- phase B: pair row max, lazy rescale, P of this wave's keys -> the pair's P buffer
@@ -873,11 +877,15 @@ void coatt_fused3_k(FusedArgs a) {
       bf16x4 v4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v4[i] = (bf16)pv[qb][i];
+      // the PV B operand's k order (the V^T fragments' key order, as the 4-wave kernel's P
+      // registers): k-step sk, lane half h, element 4a + i <-> key 16 sk + 8 a + 4 h + i.  So
+      // key 16 hb + 4 g4 + i lands in chunk 2 hb + (g4 & 1), element 4 (g4 >> 1) + i.
       const int q = 16 * qb + c16;
-      const int chunk = (2 * hb + (g4 >> 1)) ^ ((q >> 2) & 3);
-      *(bf16x4*)(pbuf + q * 64 + (chunk << 4) + 8 * (g4 & 1)) = v4;
+      const int chunk = (2 * hb + (g4 & 1)) ^ ((q >> 2) & 3);
+      *(bf16x4*)(pbuf + q * 64 + (chunk << 4) + 8 * (g4 >> 1)) = v4;
     }
     wait_t1(t, false);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier_f();
 
     // ---- phase C: O^T[this half] += V^T P^T over all 32 keys; refill tile t+3
@@ -930,6 +938,7 @@ void coatt_fused3_k(FusedArgs a) {
       v += __shfl_xor(v, 32, 64);
       if (g4 == 0) xmine[16 * qb + c16] = v;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier_f();
     lo = xmine[r] + xpart[r];
   }

@@ -382,9 +382,18 @@ __device__ __forceinline__ void raw_barrier() {
 // kt-1 -- the phase whose lgkmcnt wait retired that group's last reads of tile kt-1 (a 2-stage
 // ring refills in the first phase instead, and retires the third phase's reads before its
 // barrier).
+//
+// PP == 2 (KSG, K-split wave groups; bf16 KC operands): 2 x WM x WN waves.  Group g (waves
+// g*WM*WN ..) runs k-piece g (32 of the tile's 64 k) of every K step on the WHOLE WM x WN tile
+// layout, i.e. each wave owns a wave tile twice the size it would have with 8 waves splitting the
+// block tile, and reads half as many fragments per MFMA: LDS fragment bytes per FLOP scale as
+// 1/TM + 1/TN (the DMA-write / ds_read contention the fill probe measures), while
+// two waves per SIMD remain.  The groups' partial accumulators are summed once, in the epilogue
+// (group 1 stages its tile in LDS, group 0 adds its own before the stores).
 template <class T, class CT, int BM, int BN, int WM, int WN, int S, int LA, int LB, int EPI = 0, int PP = 0>
-__global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128 && S == 2) ? 4 : 1) void gemm_kernel(GemmArgs p) {
-  constexpr int NT = WM * WN * 64;
+__global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T) == 2 && BM * BN <= 128 * 128 && S == 2) ? 4 : 1) void gemm_kernel(GemmArgs p) {
+  constexpr bool KSG = PP == 2;
+  constexpr int NT = WM * WN * 64 * (KSG ? 2 : 1);
   constexpr int VEC = VecOf<T>::N;
   constexpr int BK = 8 * VEC;
   constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
@@ -400,7 +409,10 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
   __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
+  const int kg = KSG ? wave / (WM * WN) : 0;            // KSG: this wave's k piece
+  const int wl = KSG ? wave % (WM * WN) : wave;
+  const int wm = wl / WN, wn = wl % WN;
+  static_assert(!KSG || (sizeof(T) == 2 && !AMC && !BMC), "KSG: bf16 k-contiguous operands");
   // XCD-aware tile order (guide §5.5 T1, bijective form): blocks are dealt round-robin over
   // the 8 XCDs, so remap the linear id to give every XCD a contiguous run of M-tiles that
   // share the same B (weight) panel in its private L2.
@@ -498,7 +510,8 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
       return;
     }
 #pragma unroll
-    for (int pc = 0; pc < 2; ++pc) {
+    for (int pcl = 0; pcl < (KSG ? 1 : 2); ++pcl) {
+      const int pc = KSG ? kg : pcl;
       if constexpr (sizeof(T) == 2) {
         bf16x8 af[RM], bfr[RN];
 #pragma unroll
@@ -554,7 +567,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
     constexpr int NXT = (STG + S - 1) % S;
     const char* As = smem + STG * STAGE;
     const char* Bs = As + ABYTES;
-    if constexpr (sizeof(T) == 2 && (AMC || BMC) && (RM + RN) <= 8) {
+    if constexpr (sizeof(T) == 2 && (AMC || BMC) && (RM + RN) <= 8 && !KSG) {
       // Transposed (MC) fragments are read with ds_read_b64_tr_b16, which hipcc cannot
       // disambiguate from an in-flight LDS-DMA: a DMA issued before these reads would cost a
       // full vmcnt(0) drain in front of them.  So read the whole tile's fragments FIRST, then
@@ -591,7 +604,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
     wait_tiles<G>(min(nt - 1, kt + S - 1) - (kt + 1));
     raw_barrier();
   };
-  constexpr bool PPK = PP && sizeof(T) == 2 && !AMC && !BMC && WM * WN == 8;
+  constexpr bool PPK = PP == 1 && sizeof(T) == 2 && !AMC && !BMC && WM * WN == 8;
   if constexpr (PPK) {
     const bool g1 = __builtin_amdgcn_readfirstlane(wave) >= 4;   // waves w, w + 4 share a SIMD
     auto phase_mma = [&](const bf16x8 (&af)[RM], const bf16x8 (&bfr)[RN]) {
@@ -666,6 +679,7 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
                    : ((BM / 2) * LDC * 4 <= S * STAGE) ? BM / 2
                    : ((BM / 4) * LDC * 4 <= S * STAGE) ? BM / 4 : BM / 8;
   static_assert(HR % 16 == 0 && HR * LDC * 4 <= S * STAGE, "epilogue staging must fit in the LDS image");
+  static_assert(!KSG || HR == BM, "KSG sums the two groups' tiles in one staging pass");
   float* cs = (float*)smem;
   float alpha = p.alpha;
   if (p.scale_a) alpha *= *p.scale_a;
@@ -719,15 +733,25 @@ __global__ __launch_bounds__(WM * WN * 64, (EPI && sizeof(T) == 2 && BM * BN <= 
     }
     {
       const int g = lane >> 4;
+      // KSG: group 1 stages its partial tile, group 0 adds its own on top (one pass: HR == BM)
 #pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int rb = wm * TM + i * 16 - pass * HR;  // block's first row within this pass
-        if (rb < 0 || rb >= HR) continue;
+      for (int grp = 0; grp < (KSG ? 2 : 1); ++grp) {
+        if (!KSG || kg == 1 - grp) {
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
+          for (int i = 0; i < RM; ++i) {
+            const int rb = wm * TM + i * 16 - pass * HR;  // block's first row within this pass
+            if (rb < 0 || rb >= HR) continue;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            cs[(rb + 4 * g + r) * LDC + wn * TN + j * 16 + (lane & 15)] = acc[i][j][r] * alpha;
+            for (int j = 0; j < RN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float* c = &cs[(rb + 4 * g + r) * LDC + wn * TN + j * 16 + (lane & 15)];
+                if (KSG && grp == 1) *c += acc[i][j][r] * alpha;
+                else *c = acc[i][j][r] * alpha;
+              }
+          }
+        }
+        if (KSG && grp == 0) __syncthreads();
       }
     }
     __syncthreads();
@@ -901,6 +925,13 @@ static constexpr TileCfg kCfg[] = {
     {256, 128, 4, 2, 3, 1},  // 18: ping-pong, 8 waves of 64x64
     {128, 256, 2, 4, 3, 1},  // 19: ping-pong, 8 waves of 64x64
     {256, 256, 2, 4, 2, 1},  // 20: ping-pong, 8 waves of 128x64
+    // round 4: 4 waves (one per SIMD) with larger wave tiles -- fewer LDS fragment bytes per FLOP
+    // (1/TM + 1/TN), the contention the fill probe measures
+    {128, 256, 2, 2, 3},  // 21: 4 waves of 64x128
+    {256, 128, 2, 2, 3},  // 22: 4 waves of 128x64
+    {256, 256, 2, 2, 2},  // 23: 4 waves of 128x128
+    {128, 256, 1, 4, 3, 2},  // 24: KSG, 2 groups x 4 waves of 128x64
+    {128, 256, 2, 2, 3, 2},  // 25: KSG, 2 groups x 4 waves of 64x128
 };
 constexpr int kNumCfg = sizeof(kCfg) / sizeof(kCfg[0]);
 static int g_force_cfg = -1;
@@ -952,7 +983,7 @@ static int launch_c(const GemmArgs& a, int batch, hipStream_t st) {
   constexpr TileCfg c = kCfg[C];
   dim3 grid((a.M + c.bm - 1) / c.bm, (a.N + c.bn - 1) / c.bn, batch * a.nsplit);
   hipLaunchKernelGGL((gemm_kernel<T, CT, c.bm, c.bn, c.wm, c.wn, c.s, LA, LB, EPI, c.pp>), grid,
-                     dim3(c.wm * c.wn * 64), 0, st, a);
+                     dim3(c.wm * c.wn * 64 * (c.pp == 2 ? 2 : 1)), 0, st, a);
   CN_CHECK_LAUNCH();
   return 0;
 }
@@ -973,6 +1004,10 @@ static int launch_epi(const GemmArgs& a, hipStream_t st) {
       case 18: return launch_c<T, T, 18, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 19: return launch_c<T, T, 19, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 20: return launch_c<T, T, 20, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 21: return launch_c<T, T, 21, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 22: return launch_c<T, T, 22, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 24: return launch_c<T, T, 24, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 25: return launch_c<T, T, 25, LA, L_KC_DENSE, EPI>(a, 1, st);
       default: return CN_ERR_UNSUPPORTED;
     }
   }
@@ -1002,6 +1037,18 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 15: return launch_c<T, CT, 15, LA, LB>(a, batch, st);
       case 16: return launch_c<T, CT, 16, LA, LB>(a, batch, st);
       case 17: return launch_c<T, CT, 17, LA, LB>(a, batch, st);
+      case 21: return launch_c<T, CT, 21, LA, LB>(a, batch, st);
+      case 22: return launch_c<T, CT, 22, LA, LB>(a, batch, st);
+      case 23: return launch_c<T, CT, 23, LA, LB>(a, batch, st);
+      case 24: case 25: {  // K-split wave groups: k-contiguous operands only
+        constexpr bool kc = LA != L_MC_DENSE && LA != L_MC_CONV && LB != L_MC_DENSE && LB != L_MC_CONV;
+        if constexpr (kc) {
+          if (pick_cfg(a, batch) == 24) return launch_c<T, CT, 24, LA, LB>(a, batch, st);
+          return launch_c<T, CT, 25, LA, LB>(a, batch, st);
+        } else {
+          return launch_c<T, CT, 11, LA, LB>(a, batch, st);
+        }
+      }
       case 18: case 19: case 20: {  // ping-pong tiles: k-contiguous operands only
         constexpr bool kc = LA != L_MC_DENSE && LA != L_MC_CONV && LB != L_MC_DENSE && LB != L_MC_CONV;
         if constexpr (kc) {

@@ -3,7 +3,8 @@ cn_gemm_force_config) on the operand kinds the heuristic can route to it: conv f
 dense and 3x3 gathered loaders), stride-1 dgrad, the BN-statistics and BN-backward epilogues,
 and the weight gradient (transposed loaders; the ping-pong ids fall back there) -- against torch
 fp64, at shapes whose M, N and K all end in partial tiles.  The ping-pong tiles (ids 18-20)
-change the K loop's synchronisation, so each is also run several times on the same inputs and
+change the K loop's synchronisation (and 24-25, the K-split wave groups, sum two partial
+accumulators), so each is also run several times on the same inputs and
 must give bitwise-identical results (a fragment read racing an LDS-DMA fill shows up as
 run-to-run differences)."""
 import pytest
@@ -15,8 +16,8 @@ import test_gpu_kernels as K
 
 pytestmark = pytest.mark.gpu
 
-CFGS = [11, 13, 10, 15, 4, 18, 19, 20]
-EPI_CFGS = {10, 11, 12, 13, 18, 19, 20}   # the tiles launch_epi instantiates
+CFGS = [11, 13, 10, 15, 4, 18, 19, 20, 21, 22, 23, 24, 25]
+EPI_CFGS = {10, 11, 12, 13, 18, 19, 20, 21, 22, 24, 25}   # the tiles launch_epi instantiates
 
 
 @pytest.fixture
@@ -42,7 +43,7 @@ def test_conv_paths_per_config(cuda, force_cfg, cfg):
         K.test_conv_dgrad_bn_epilogue_reduce(cuda, bf, case)
 
 
-@pytest.mark.parametrize("cfg", [18, 19, 20])
+@pytest.mark.parametrize("cfg", [18, 19, 20, 24, 25])
 def test_ping_pong_tiles_are_deterministic(cuda, force_cfg, cfg):
     from cosnet_amd import ops
     force_cfg(cfg)
