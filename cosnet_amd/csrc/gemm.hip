@@ -929,7 +929,7 @@ static constexpr TileCfg kCfg[] = {
     // (1/TM + 1/TN), the contention the fill probe measures
     {128, 256, 2, 2, 3},  // 21: 4 waves of 64x128
     {256, 128, 2, 2, 3},  // 22: 4 waves of 128x64
-    {256, 256, 2, 2, 2},  // 23: 4 waves of 128x128
+    {256, 256, 2, 2, 2},  // 23: (4 waves of 128x128 spill 36-151 VGPRs; launches config 10)
     {128, 256, 1, 4, 3, 2},  // 24: KSG, 2 groups x 4 waves of 128x64
     {128, 256, 2, 2, 3, 2},  // 25: KSG, 2 groups x 4 waves of 64x128
 };
@@ -967,7 +967,9 @@ static int heuristic_cfg(int M, int N, int K, int bz) {
   }
   if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 20;
   if (tiles_of(11, M, N) * bz <= 256 && K >= 512) return 13;
-  if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return 19;
+  // CN_GEMM_N256 overrides the tile of these products (A/B runs: 19, 11, 24, 25)
+  static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); return e ? atoi(e) : 19; }();
+  if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return n256;
   if (N >= 1024 && K <= 512 && tiles_of(10, M, N) * bz >= 200) return 10;
   return 11;
 }
@@ -1039,7 +1041,7 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 17: return launch_c<T, CT, 17, LA, LB>(a, batch, st);
       case 21: return launch_c<T, CT, 21, LA, LB>(a, batch, st);
       case 22: return launch_c<T, CT, 22, LA, LB>(a, batch, st);
-      case 23: return launch_c<T, CT, 23, LA, LB>(a, batch, st);
+      case 23: return launch_c<T, CT, 10, LA, LB>(a, batch, st);   // 4 waves of 128x128 spill: not built
       case 24: case 25: {  // K-split wave groups: k-contiguous operands only
         constexpr bool kc = LA != L_MC_DENSE && LA != L_MC_CONV && LB != L_MC_DENSE && LB != L_MC_CONV;
         if constexpr (kc) {

@@ -2,14 +2,18 @@
 
 The fp8 path changes the forward conv GEMM operands (e4m3), the dgrad operands of the
 compute-heavy convs (e5m2 output gradients x e4m3 transposed weights) and -- for the no-grad
-co-attention -- the affinity / gather operands (cosnet_amd/fp8.py), so its parity is
-statistical.  Over 4 seeded SGD steps at 97x97 (B = 2 pairs), each on a
-different seeded batch: the mean fp8 loss within 8 % of the mean bf16 loss, every step within
-25 % (a blow-up guard: e4m3 keeps 3 mantissa bits and this random-init 101-layer net is chaotic
-in low precision -- the step-0 gap, same weights, is the forward's precision alone, 4-5 %; later
-steps measured 2-18 %, and move with any reordering of the bf16 run's fp32 sums), and the output
-maps' means within 0.05.  The kernels themselves are pinned exactly in test_gpu_kernels.py
-(test_fp8_quant_matches_torch_e4m3fn, test_conv_fwd_fp8).
+co-attention -- the affinity / gather operands (cosnet_amd/fp8.py); the training co-attention
+stays the bf16 flash pair, so its gradient is the gradient of its forward.  Parity is
+statistical, with the bounds DESIGN §3.5 states: over 4 seeded SGD steps
+at 97x97 (B = 2 pairs), each on a different seeded batch, the mean fp8 loss within 5 % of the
+mean bf16 loss, every step within 15 %, the step-0 gap (same weights: the forward's precision
+alone) within 8 %, and the output maps' means within 0.03.  The distribution these bounds are
+set against, 5 seeds x {fp32, bf16, fp8} (tools/fp8_curve_dist.py, profiles/r04_fp8_curve_dist.json):
+mean gap 1.0-4.0 % (median 1.8 %), per-step gap median 4.1 %, p90 7.9 %, max 14.7 %, map-mean gap
+<= 0.026 -- while bf16 itself is up to 18 % per step and 0.032 in map mean away from fp32 on the
+same batches (this random-init 101-layer net is chaotic in low precision).  The kernels
+themselves are pinned exactly in test_gpu_kernels.py (test_fp8_quant_matches_torch_e4m3fn,
+test_conv_fwd_fp8).
 """
 import numpy as np
 import pytest
@@ -54,15 +58,10 @@ def test_fp8_training_loss_curve_tracks_bf16(cuda):
     l8, m8, model = _run(cuda, True, False)
     assert np.isfinite(l8).all()
     rel = np.abs(l8 - l16) / np.abs(l16)
-    # mean gap 8 %: the per-step gaps are 2-18 % (chaotic net, see above), so the 4-step mean
-    # moves by a few % with any reordering of fp32 sums -- round 3's row-aligned weight-gradient
-    # K order alone moved it from 4.6 to 5.8 % with the fp8 path itself unchanged, and the bf16
-    # run's split-K ASPP bottleneck conv moved step 1 from 13 to 18 % (mean 4.0 %)
+    # this seed (100) in the committed distribution: step gaps 4.3 / 7.5 / 6.7 / 3.6 %, mean 1.3 %
     assert rel[0] <= 0.08, (l8, l16)     # same weights: the forward's precision alone
-    assert abs(l8.mean() - l16.mean()) <= 0.08 * l16.mean() and (rel <= 0.25).all(), (l8, l16)
-    # output-map means after the 4 steps: 0.05 (measured 0.012 / 0.031 with e5m2 dgrads on top of
-    # the e4m3 forward; 0.01-0.02 with the forward alone)
-    assert abs(m8[0] - m16[0]) <= 0.05 and abs(m8[1] - m16[1]) <= 0.05, (m8, m16)
+    assert abs(l8.mean() - l16.mean()) <= 0.05 * l16.mean() and (rel <= 0.15).all(), (l8, l16)
+    assert abs(m8[0] - m16[0]) <= 0.03 and abs(m8[1] - m16[1]) <= 0.03, (m8, m16)
     ctx = model.fp8
     assert len(ctx.weights._c) > 100 and len(ctx.acts.slots) > 50   # the encoders ran fp8
     assert len(ctx.grads.slots) >= 20                                # and their dgrads (e5m2)

@@ -20,7 +20,7 @@ template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
 }
 
-template <int TILE, int NS, int NT>
+template <int TILE, int NS, int NT, bool DMA = true>
 __global__ __launch_bounds__(NT) void fill_k(const char* src, long long span, long long bstride, int ntiles,
                                              int R, float* sink) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -31,6 +31,7 @@ __global__ __launch_bounds__(NT) void fill_k(const char* src, long long span, lo
   __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000);
   char* wb = lds + __builtin_amdgcn_readfirstlane((tid & ~63) * 16);
   auto issue = [&](int t, int stage) {
+    if (!DMA) return;
     const long long off = (base + (long long)t * TILE) % (span - TILE + 1);
     const unsigned soff = (unsigned)(off & ~15ll);
 #pragma unroll
@@ -46,9 +47,13 @@ __global__ __launch_bounds__(NT) void fill_k(const char* src, long long span, lo
     const int st = t % NS;
     if (t + NS - 1 < ntiles) issue(t + NS - 1, (t + NS - 1) % NS);
     const char* sp = lds + st * TILE;
-    for (int r = 0; r < R; ++r) {
-      const u32x4 v = *(const u32x4*)(sp + ((r * 64 + lane) * 16) % TILE);
-      acc ^= v;
+    // fragment-like reads: 8 in flight, then folded (a GEMM's prefetched fragment reads)
+    for (int r0 = 0; r0 < R; r0 += 8) {
+      u32x4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = *(const u32x4*)(sp + (((r0 + q) * 64 + lane) * 16) % TILE);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) if (r0 + q < R) acc ^= v[q];
     }
     if (t + NS - 1 < ntiles) wait_vm<CH * (NS - 2)>();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -115,28 +120,28 @@ void run_vgpr(const char* name, const char* src, long long span, long long bstri
          bytes / us / 1e3 / 256, bytes / us / 1e6);
 }
 
-template <int TILE, int NS, int NT>
+template <int TILE, int NS, int NT, bool DMA = true>
 void run(const char* name, const char* src, long long span, long long bstride, int ntiles, int R, float* sink) {
   const size_t shm = (size_t)NS * TILE < 98304 ? 98304 : (size_t)NS * TILE;
-  hipFuncSetAttribute((const void*)fill_k<TILE, NS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  hipFuncSetAttribute((const void*)fill_k<TILE, NS, NT, DMA>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   for (int rep = 0; rep < 2; ++rep)
-    hipLaunchKernelGGL((fill_k<TILE, NS, NT>), dim3(256), dim3(NT), shm, 0, src, span, bstride, ntiles, R, sink);
+    hipLaunchKernelGGL((fill_k<TILE, NS, NT, DMA>), dim3(256), dim3(NT), shm, 0, src, span, bstride, ntiles, R, sink);
   hipEventRecord(e0, 0);
   const int reps = 5;
   for (int rep = 0; rep < reps; ++rep)
-    hipLaunchKernelGGL((fill_k<TILE, NS, NT>), dim3(256), dim3(NT), shm, 0, src, span, bstride, ntiles, R, sink);
+    hipLaunchKernelGGL((fill_k<TILE, NS, NT, DMA>), dim3(256), dim3(NT), shm, 0, src, span, bstride, ntiles, R, sink);
   hipEventRecord(e1, 0);
   hipEventSynchronize(e1);
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   const double us = ms * 1e3 / reps;
   const double bytes = 256.0 * ntiles * TILE;
-  printf("%-10s tile %3d KB x %d stages (%3d KB in flight) %4d thr  R=%2d : %7.1f us  %6.1f GB/s per CU  %5.2f TB/s chip  %.3f us/tile\n",
-         name, TILE / 1024, NS, (NS - 1) * TILE / 1024, NT, R, us, bytes / us / 1e3 / 256, bytes / us / 1e6,
-         us / ntiles);
+  printf("%-10s %s tile %3d KB x %d stages (%3d KB in flight) %4d thr  R=%2d : %7.1f us  %6.1f GB/s per CU  %5.2f TB/s chip  %.3f us/tile\n",
+         name, DMA ? "dma" : "---", TILE / 1024, NS, (NS - 1) * TILE / 1024, NT, R, us, bytes / us / 1e3 / 256,
+         bytes / us / 1e6, us / ntiles);
 }
 
 int main(int argc, char** argv) {
@@ -150,6 +155,19 @@ int main(int argc, char** argv) {
   // weights: every block streams the same 1.2 MB (layer-3 3x3 weights); activations: block-private
   // runs of a 60 MB tensor (MALL) and of a 1 GB buffer (HBM)
   const Src srcs[] = {{"shared1M", 1179648, 0}, {"priv60M", 60ll << 20, 240 << 10}, {"priv1G", big, 4ll << 20}};
+  // round 4b: DMA only / reads only / both, shared (L2-resident) source; R = ds_read_b128 per wave
+  // per tile (the 128x256 GEMM tile reads 16 per wave per K step, 256x256: 24)
+  if (argc > 1) {
+    const Src& s = srcs[0];
+    for (int R : {0, 8, 16, 24}) {
+      run<49152, 3, 512, true>(s.name, src, s.span, s.bstride, 36, R, sink);
+      run<49152, 3, 512, false>(s.name, src, s.span, s.bstride, 36, R, sink);
+      run<65536, 2, 512, true>(s.name, src, s.span, s.bstride, 36, R, sink);
+    }
+    hipFree(src);
+    hipFree(sink);
+    return 0;
+  }
   for (const Src& s : srcs) {
     const int nt48 = 36;   // K steps of the layer-3 3x3 conv
     run<49152, 3, 512>(s.name, src, s.span, s.bstride, nt48, 0, sink);
