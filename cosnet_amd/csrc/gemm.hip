@@ -967,8 +967,10 @@ static int heuristic_cfg(int M, int N, int K, int bz) {
   }
   if (N >= 512 && K >= 2048 && tiles_of(10, M, N) * bz >= 200) return 20;
   if (tiles_of(11, M, N) * bz <= 256 && K >= 512) return 13;
-  // CN_GEMM_N256 overrides the tile of these products (A/B runs: 19, 11, 24, 25)
-  static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); return e ? atoi(e) : 19; }();
+  // Round 4: 128x128 / 8 waves for these products (layer-3 3x3 fwd 38 vs 46 us, 1x1 fwd 22 vs 25
+  // us isolated; whole step +0.2 %: profiles/r04_gemm_n256_tiles_ab.txt).  CN_GEMM_N256 overrides
+  // it for A/B runs (19 = the round-3 128x256 ping-pong, 24 / 25 = K-split wave groups).
+  static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); return e ? atoi(e) : 11; }();
   if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return n256;
   if (N >= 1024 && K <= 512 && tiles_of(10, M, N) * bz >= 200) return 10;
   return 11;
