@@ -25,7 +25,7 @@ sys.path.insert(0, REPO)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(REPO, "profiles", "r03_pmc_step_traffic.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r04_pmc_step_traffic.json")
 ROCPROF_FILE = os.path.join(REPO, "profiles", "r04_rocprof_kernel_stats_bench_b4_473.csv")
 
 
