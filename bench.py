@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--fp32-extra", type=int, default=1,
                     help="also time a few recorded fp32 steps (full-precision throughput beside "
                          "the bf16 headline; N = 1 only)")
+    ap.add_argument("--fp8-extra", type=int, default=1,
+                    help="also time a few recorded steps of BASELINE configs[4]'s per-GPU fp8 "
+                         "workload (8 pairs; N = 1 only)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
@@ -202,16 +205,21 @@ def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):
             "executed_tflops": 4 / 3 * alg / t / 1e12, "us_per_launch": t * 1e6}
 
 
-def fp32_extra(dev, B, S, steps=5, warmup=2):
-    """Full-precision throughput beside the bf16 headline: the same recorded train step in fp32
-    (every GEMM on the f32 MFMA, 157 TFLOP/s peak), `steps` timed replays after `warmup`."""
+def extra_line(dev, B, S, kind, steps=5, warmup=2):
+    """A second precision beside the bf16 headline, the same recorded train step timed over
+    `steps` replays after `warmup`:
+      fp32 -- every GEMM on the f32 MFMA (157 TFLOP/s peak), B pairs;
+      fp8  -- BASELINE configs[4]'s per-GPU step (8 pairs, 64 over 8 GPUs): e4m3 forward convs,
+              e5m2 dgrads, bf16 weight gradients and co-attention training kernels."""
     import torch
     import cosnet_amd as C
     from cosnet_amd.init_recipe import recipe_state_dict, synthetic_inputs
     from cosnet_amd.optim import SGD, reference_param_groups
     from cosnet_amd.train_step import TrainStep
-    m = C.build_model(torch.float32)
+    m = C.build_model(torch.float32 if kind == "fp32" else torch.bfloat16)
     m.load_state_dict(recipe_state_dict(m.state_dict()))
+    if kind == "fp8":
+        m.set_fp8(True)
     m.encoder.main_classifier.requires_grad_(False)
     m = m.to(dev).train()
     g0, g1 = reference_param_groups(m)
@@ -226,10 +234,11 @@ def fp32_extra(dev, B, S, steps=5, warmup=2):
         loss = st([2.5e-6, 2.5e-3])
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    out = {"value": B * steps / dt, "unit": "frame-pairs/s", "dtype": "fp32", "steps": steps,
-           "ms_per_step": dt / steps * 1e3, "loss": float(loss.item()),
-           "model_tflops_per_s": B * steps * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
-           "peak_tflops": MFMA_F32_PEAK_TFLOPS}
+    out = {"value": B * steps / dt, "unit": "frame-pairs/s", "dtype": kind, "batch": B,
+           "steps": steps, "ms_per_step": dt / steps * 1e3, "loss": float(loss.item()),
+           "model_tflops_per_s": B * steps * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None}
+    if kind == "fp32":
+        out["peak_tflops"] = MFMA_F32_PEAK_TFLOPS
     del st, opt, m
     torch.cuda.empty_cache()
     return out
@@ -478,7 +487,10 @@ def main():
                              "source": tr["source"]}
     if args.fp32_extra and dtype == torch.bfloat16 and world == 1 and not args.no_roofline:
         log("fp32 extra ...")
-        out["fp32_extra"] = fp32_extra(dev, B, S)
+        out["fp32_extra"] = extra_line(dev, B, S, "fp32")
+    if args.fp8_extra and args.dtype == "bf16" and world == 1 and not args.no_roofline and S == 473:
+        log("fp8 extra (configs[4] per-GPU batch 8) ...")
+        out["fp8_extra"] = extra_line(dev, 8, S, "fp8")
     out["build"] = __import__("cosnet_amd._native", fromlist=["build_info"]).build_info()
     if rank == 0 and args.cpu_baseline and world == 1:
         log("cpu baseline ...")
