@@ -135,8 +135,8 @@ def load():
 
 
 HASHED_SOURCES = ["gemm.hip", "conv.hip", "bn.hip", "ew.hip", "coatt.hip", "coatt_fused.hip",
-                  "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip", "common.h", "gemm.h",
-                  "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
+                  "coatt_dsplit.hip", "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip",
+                  "common.h", "gemm.h", "coatt_fused.h", "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
 
 
 def source_hash():

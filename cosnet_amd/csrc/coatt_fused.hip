@@ -26,17 +26,12 @@
 #include "common.h"
 #include <cstdlib>
 #include "../../include/cosnet_hip.h"
+#include "coatt_fused.h"
 
 namespace {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
-constexpr int FD = 256;              // feature channels (all_channel)
-constexpr int FBQ = 128;             // query rows per workgroup
-constexpr int FBK = 32;              // keys per tile
-constexpr int FROWB = FD * 2;        // bytes per key row in LDS
-constexpr int FTILE = FBK * FROWB;   // 16 KB per K (or V) tile
-constexpr int FQB = FBQ * FROWB;     // 64 KB Q block
 constexpr int FSTAGES = 3;           // K/V ring depth (two tiles in flight behind the one read)
 constexpr int FDMA = 2 * FTILE / 4096;  // LDS-DMA instructions per thread per K/V tile
 #ifndef CF_KPF
@@ -64,27 +59,6 @@ __device__ __forceinline__ void raw_barrier_f() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-
-struct FusedDir {
-  const bf16* q; const bf16* k; const bf16* v; bf16* o;
-  long long ldq, ldk, ldv, ldo;
-  float* lse;          // MODE 0 (optional): log2-sum-exp2 of each query row's logits x log2(e),
-                       //   [B][HWp] (rows HW..HWp-1 get +inf)
-  const float* klse;   // MODE 1: per-KEY normaliser in the same units, [B][HWp], +inf padded
-};
-struct FusedArgs {
-  FusedDir dir[2];
-  int HW, HWp, ndir, nrb, nwork, accumulate;
-  // tail key split (MODE 0, no-grad forward).  Items = (row block, batch x direction); the
-  // first nfull items run whole, one workgroup each (full rounds of the chip); each of the
-  // remaining items is split over nsplit workgroups, split s covering key tiles
-  // [s tps, (s+1) tps), which write their un-normalised O (fp32) and row (max, sum) to the
-  // partials that coatt_merge_k folds in split order -- the last, partial round of workgroups
-  // becomes a short round of short workgroups.
-  int nitems, nfull, nsplit, tps;
-  float* opart;    // [nsplit][nitems - nfull][128][256]
-  float* mlpart;   // [nsplit][nitems - nfull][128][2]
-};
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
@@ -1059,23 +1033,24 @@ static void plan_split(int items, int ntiles, int* nfull, int* nsplit) {
 }
 
 // Kernel variant: 1 = coatt_fused_fwd_k (4 waves, one per SIMD), 2 = coatt_fused2_k (wave pairs,
-// duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys).  CN_COATT_VARIANT picks the
+// duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys), 4 = coatt_dsplit_k
+// (coatt_dsplit.hip: wave pairs splitting the channels, 64 query rows per pair).  CN_COATT_VARIANT picks the
 // default; cn_coatt_force_variant overrides it (tests, A/B tools).
 static int g_coatt_variant = 0;
 static int coatt_variant() {
   static const int v = [] {
     const char* e = getenv("CN_COATT_VARIANT");
     const int x = e ? atoi(e) : 1;
-    return (x >= 1 && x <= 3) ? x : 1;
+    return (x >= 1 && x <= 4) ? x : 1;
   }();
   return g_coatt_variant ? g_coatt_variant : v;
 }
 
-// Development / test hook: force the forward / PV kernel variant (1, 2, 3 as above; 0: default).
+// Development / test hook: force the forward / PV kernel variant (1..4 as above; 0: default).
 // Returns the previous setting.
 extern "C" int cn_coatt_force_variant(int v) {
   const int old = g_coatt_variant;
-  g_coatt_variant = (v >= 1 && v <= 3) ? v : 0;
+  g_coatt_variant = (v >= 1 && v <= 4) ? v : 0;
   return old;
 }
 
@@ -1096,6 +1071,9 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   } else if (var == 3) {
     if (mode == 0) hipLaunchKernelGGL(coatt_fused3_k<0>, grid, dim3(F2NT), 0, st, a);
     else hipLaunchKernelGGL(coatt_fused3_k<1>, grid, dim3(F2NT), 0, st, a);
+  } else if (var == 4) {
+    const int rc = coatt_dsplit_launch(mode, a, grid, st);
+    if (rc) return rc;
   } else {
     if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);

@@ -198,10 +198,13 @@ def test_paired_wave_kernel_is_bitwise_the_four_wave_kernel(cuda, n, hw):
         assert torch.equal(x, y), (k, (x.float() - y.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("var", [3, 4])
 @pytest.mark.parametrize("n,hw", [(1, 1), (2, 63), (1, 97), (2, 169), (1, 1271), (4, 3600), (5, 3600)])
-def test_key_split_pair_kernel(cuda, n, hw):
-    """The 8-wave forward whose wave pairs split the keys of S (coatt_fused3_k, 16x16x32 S
-    products, pair-wise max / P exchange through LDS) against fp64 of rgbd_segmentation_RAA.py:
+def test_split_pair_kernels(cuda, n, hw, var):
+    """The wave-pair forward / PV kernels that split S between the two waves of a pair --
+    variant 3 (coatt_fused3_k, 8 waves: the keys, 16x16x32 S products, pair-wise max / P
+    exchange through LDS) and variant 4 (coatt_dsplit_k, 4 waves: the channels, 64 query rows
+    per pair, partial S exchanged and added) -- against fp64 of rgbd_segmentation_RAA.py:
     160-170 (no-grad forward incl. the key-split tail), and against the 4-wave kernel: training
     forward's LSE to 1e-4 (only S's summation order differs) and the PV backward kernel within
     the bf16 output rounding."""
@@ -212,7 +215,7 @@ def test_key_split_pair_kernel(cuda, n, hw):
     outs = []
     old = lib.cn_coatt_force_variant(1)
     try:
-        for v in (1, 3):
+        for v in (1, var):
             lib.cn_coatt_force_variant(v)
             za, zb = ops.coatt_fused(vat, va, vb, n, hw, torch.empty_like(va), torch.empty_like(va))
             la = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=cuda)
