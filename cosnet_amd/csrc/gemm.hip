@@ -972,7 +972,10 @@ static int heuristic_cfg(int M, int N, int K, int bz) {
   // it for A/B runs (19 = the round-3 128x256 ping-pong, 24 / 25 = K-split wave groups).
   static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); return e ? atoi(e) : 11; }();
   if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return n256;
-  if (N >= 1024 && K <= 512 && tiles_of(10, M, N) * bz >= 200) return 10;
+  // shallow wide products (1x1 convs with K <= 512 into >= 1024 channels): 256x256 by the
+  // round-3 isolated sweep; CN_GEMM_SHALLOW overrides it for in-step A/B runs
+  static const int shallow = [] { const char* e = getenv("CN_GEMM_SHALLOW"); return e ? atoi(e) : 10; }();
+  if (N >= 1024 && K <= 512 && tiles_of(10, M, N) * bz >= 200) return shallow;
   return 11;
 }
 
