@@ -378,7 +378,9 @@ int cn_gemm_force_config(int cfg);
 int cn_gemm_set_wgrad_target(int blocks);
 /* Development / test hook: co-attention flash forward and PV kernel variant (1: four waves, one
  * per SIMD; 2: eight waves in pairs that split the output channels, S computed by both; 3: pairs
- * that split the keys of S and the output channels; 0: default).  Returns the previous setting. */
+ * that split the keys of S and the output channels; 4: four waves in pairs of 64 query rows that
+ * split the channels of S (partial S exchanged through LDS) and of the output; 0: default).
+ * Returns the previous setting.  CN_COATT_VARIANT sets the default. */
 int cn_coatt_force_variant(int v);
 
 #ifdef __cplusplus
