@@ -349,8 +349,10 @@ extern "C" int cn_gemm_set_wgrad_target(int blocks) {
   return 0;
 }
 
+// G > 1: the split for G problems of this shape in one launch (cn_conv_wgrad_grouped_ws), the
+// block target shared by the G problems.
 static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int KW, int Cin, int* nsplit,
-                       int* chunk, int* cfg) {
+                       int* chunk, int* cfg, int G = 1) {
   int M = Cout, NN = KH * KW * Cin, K = N * OH * OW;
   int BK = 8 * vec_of(dtype);
   long long tiles;
@@ -359,7 +361,7 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
     // 128x128 / 8 waves (tools/wgrad_sweep.sh); the narrow layer-1 products get tiles that
     // do not waste half their MFMAs: 128x64 for N <= 64, 64x128 for Cout <= 64
     *cfg = NN <= 64 ? 12 : (M <= 64 ? 17 : 11);
-    tiles = cn_gemm_cfg_blocks(*cfg, M, NN);
+    tiles = cn_gemm_cfg_blocks(*cfg, M, NN) * G;
     // split count from a per-split sweep on the step's shapes (tools/wgrad_bench.py,
     // profiles/r03_wgrad_splits.txt): up to 512 blocks = two co-resident blocks per CU, never a
     // third round (layer-3 3x3: 8 -> 14 splits 44.6 -> 37.0 us, layer-4 3x3: 2 -> 3 splits
@@ -472,6 +474,93 @@ extern "C" int cn_conv_wgrad_grouped(int dtype, int G, const void* const* xs, lo
     if (a.M <= 64) a.cfg = 17;
   }
   return cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);
+}
+
+// ---- grouped weight gradients split over K --------------------------------------------------
+// The small bottleneck weight gradients (layers 1-2: 8-36 tiles per problem) fill the chip
+// neither one by one (100-225 blocks each, plus a reduce launch each) nor grouped without a
+// split (G x 8-36 blocks running K = all pixels).  Here G problems x nsplit K chunks run as ONE
+// launch (blockIdx.z = problem x split; slabs ws[g][s][Cout*KH*KW*Cin], plain stores), then ONE
+// reduce launch sums every problem's slabs in split order (deterministic) into its dW.
+namespace {
+struct RedOut { float* out[GEMM_MAXG]; };
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_k(const float* __restrict__ ws, int nsplit,
+                                                               long long slab, long long n4, RedOut o) {
+  const int g = blockIdx.y;
+  const float* wg = ws + (long long)g * nsplit * slab;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 8 <= nsplit; s += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(wg + (long long)(s + u) * slab + 4 * i);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; s < nsplit; ++s) a += *(const f32x4*)(wg + (long long)s * slab + 4 * i);
+    ((f32x4*)o.out[g])[i] = a;
+  }
+}
+}  // namespace
+
+extern "C" size_t cn_conv_wgrad_grouped_workspace_floats(int dtype, int G, int N, int OH, int OW,
+                                                         int Cout, int KH, int KW, int Cin) {
+  if (G < 1) return 0;
+  int ns, ch, cfg;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg, G);
+  return ns > 1 ? (size_t)G * ns * Cout * KH * KW * Cin : 0;
+}
+
+extern "C" int cn_conv_wgrad_grouped_ws(int dtype, int G, const void* const* xs, long long ldx, int N,
+                                        int H, int W, int Cin, const void* const* dys, long long lddy,
+                                        int OH, int OW, int Cout, int KH, int KW, int stride, int pad,
+                                        int dil, float* const* dws, float* ws, size_t ws_floats,
+                                        hipStream_t st) {
+  if (G < 1 || G > GEMM_MAXG) return CN_ERR_SHAPE;
+  if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
+  int ns, ch, cfg;
+  wgrad_plan(dtype, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg, G);
+  const long long slab = (long long)Cout * KH * KW * Cin;
+  if (ns <= 1 || !ws || ws_floats < (size_t)G * ns * slab || ((uintptr_t)ws & 15) || slab % 4)
+    return cn_conv_wgrad_grouped(dtype, G, xs, ldx, N, H, W, Cin, dys, lddy, OH, OW, Cout, KH, KW,
+                                 stride, pad, dil, dws, st);
+  for (int g = 0; g < G; ++g)
+    if ((uintptr_t)dws[g] & 15) return CN_ERR_ALIGN;
+  GemmArgs a = gemm_defaults();
+  a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
+  a.ka_lim = a.kb_lim = a.K;
+  a.lda = lddy;
+  a.ldb = ldx;
+  a.ldc = a.N;
+  int lb = L_MC_DENSE;
+  if (!(KH == 1 && KW == 1 && stride == 1 && pad == 0)) {
+    lb = L_MC_CONV;
+    a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  }
+  a.ngroup = G;
+  for (int g = 0; g < G; ++g) {
+    a.grp.A[g] = dys[g];
+    a.grp.B[g] = xs[g];
+    a.grp.C[g] = ws + (long long)g * ns * slab;   // problem g's slabs
+  }
+  a.A = dys[0]; a.B = xs[0]; a.C = ws;
+  a.cfg = cfg;
+  a.nsplit = ns;
+  a.k_chunk = ch;
+  a.c_mode = 3;
+  a.slab = slab;
+  int rc = cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);
+  if (rc) return rc;
+  RedOut o;
+  for (int g = 0; g < G; ++g) o.out[g] = dws[g];
+  const long long n4 = slab / 4;
+  long long bx = (n4 + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(splitk_reduce_grouped_k, dim3((unsigned)bx, G), dim3(256), 0, st, (const float*)ws,
+                     ns, slab, n4, o);
+  CN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,

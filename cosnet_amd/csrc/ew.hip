@@ -621,33 +621,18 @@ __global__ __launch_bounds__(256) void sgd_k(const SgdTensor* __restrict__ ts, i
     if (T.mode == 0) {
       if (T.wdt == 0 && (T.beg & 3) == 0 && ((T.end - T.beg) & 3) == 0 &&
           ((uintptr_t)T.p & 15) == 0 && ((uintptr_t)T.g & 15) == 0 && ((uintptr_t)T.buf & 15) == 0) {
-        // SU chunks per thread with all their loads issued before any store (the stores could
-        // alias the loads as far as the compiler knows, so it would not hoist them itself)
-        constexpr int SU = 4;
-        for (long long i0 = T.beg + 4 * tid; i0 < T.end; i0 += SU * 4 * 256) {
-          f32x4 p[SU], g[SU], b[SU];
+        for (long long i = T.beg + 4 * tid; i < T.end; i += 4 * 256) {
+          f32x4 p = *(const f32x4*)(T.p + i), g = *(const f32x4*)(T.g + i);
+          f32x4 b = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + i);
 #pragma unroll
-          for (int u = 0; u < SU; ++u) {
-            const long long i = i0 + u * 4 * 256;
-            const long long il = i < T.end ? i : T.beg;   // past the end: a valid chunk, not stored
-            p[u] = *(const f32x4*)(T.p + il);
-            g[u] = *(const f32x4*)(T.g + il);
-            b[u] = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + il);
+          for (int e = 0; e < 4; ++e) {
+            float pe = p[e], be = b[e];
+            sgd_upd(pe, g[e], be, lr, wd, mom, T.first);
+            p[e] = pe;
+            b[e] = be;
           }
-#pragma unroll
-          for (int u = 0; u < SU; ++u) {
-            const long long i = i0 + u * 4 * 256;
-            if (i >= T.end) break;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float pe = p[u][e], be = b[u][e];
-              sgd_upd(pe, g[u][e], be, lr, wd, mom, T.first);
-              p[u][e] = pe;
-              b[u][e] = be;
-            }
-            *(f32x4*)(T.p + i) = p[u];
-            *(f32x4*)(T.buf + i) = b[u];
-          }
+          *(f32x4*)(T.p + i) = p;
+          *(f32x4*)(T.buf + i) = b;
         }
       } else {
         for (long long i = T.beg + tid; i < T.end; i += 256) {
@@ -675,23 +660,13 @@ __global__ __launch_bounds__(256) void sgd_k(const SgdTensor* __restrict__ ts, i
       const int co0 = cob * 64, ci0 = cib * 64;
       const int rr = tid >> 4, c4 = (tid & 15) * 4;
       const int ci = ci0 + c4;
-      // the four rows' loads all in flight before the first store (see mode 0)
-      f32x4 pj[4], gj[4], bj[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = co0 + rr + 16 * j;
-        const bool ok = co < T.cout && ci < T.cin;
-        const long long idx = ok ? ((long long)co * T.khw + tap) * T.cin + ci : 0;
-        pj[j] = *(const f32x4*)(T.p + idx);
-        gj[j] = *(const f32x4*)(T.g + idx);
-        bj[j] = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + idx);
-      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int co = co0 + rr + 16 * j;
         if (co < T.cout && ci < T.cin) {
           const long long idx = ((long long)co * T.khw + tap) * T.cin + ci;
-          f32x4 p = pj[j], g = gj[j], b = bj[j];
+          f32x4 p = *(const f32x4*)(T.p + idx), g = *(const f32x4*)(T.g + idx);
+          f32x4 b = T.first ? (f32x4){0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(T.buf + idx);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float pe = p[e], be = b[e];

@@ -53,6 +53,9 @@ class GradSink(dict):
 # "end" (after the whole dgrad chain) or "layer" (after each layer's blocks: the queue's dY and
 # input tensors are released per layer).  CN_WGRAD_FLUSH selects it for A/B runs.
 WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
+# Small-shape groups split over K (cn_conv_wgrad_grouped_ws); CN_WGRAD_GSPLIT=0 issues them one
+# by one as split-K launches (A/B runs).
+WGRAD_GSPLIT = os.environ.get("CN_WGRAD_GSPLIT", "1") != "0"
 
 
 def _layer_index(enc):
@@ -93,6 +96,11 @@ class WgradQueue:
                 chunk = jobs[i:i + ops.GROUP_MAX]
                 if len(chunk) >= 3 and tiles * len(chunk) >= 128:
                     ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
+                elif len(chunk) >= 2 and tiles * len(chunk) < 128 and WGRAD_GSPLIT:
+                    # small shapes (layers 1-2): the group split over K as well -- one GEMM and
+                    # one reduce launch instead of a split-K GEMM + reduce per problem
+                    ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil,
+                                           split=True)
                 else:
                     for x, dy, dw in chunk:
                         conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw)

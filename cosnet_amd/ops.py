@@ -355,10 +355,12 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
 GROUP_MAX = 24       # cn_conv_wgrad_grouped's problem limit (gemm.h GEMM_MAXG)
 
 
-def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil):
+def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil, split=False):
     """Weight gradients of G convs of ONE shape in one launch (cn_conv_wgrad_grouped): jobs =
     [(x, dy, dw)] with x [n*h*w, cin], dy [n*oh*ow, cout] sharing the row strides, dw fp32
-    [cout, k*k*cin] (written).  No split-K workspace and no reduce launch."""
+    [cout, k*k*cin] (written).  No split-K workspace and no reduce launch.  split=True: the G
+    problems also split over K (cn_conv_wgrad_grouped_ws: one GEMM launch + one reduce launch
+    for the group), for shapes too small to fill the chip grouped whole."""
     import ctypes
     g = len(jobs)
     if not 1 <= g <= GROUP_MAX:
@@ -373,9 +375,17 @@ def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil):
     fl = 2.0 * n * oh * ow * cout * k * k * cin
     ev = _prof_start(g * fl, ("wgrad", cout, k * k * cin, n * oh * ow),
                      g * (es * (n * h * w * cin + n * oh * ow * cout) + 4 * cout * k * k * cin))
-    nv.call("cn_conv_wgrad_grouped", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
-            ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil, ctypes.addressof(dws),
-            nv.stream())
+    nws = int(nv.query("cn_conv_wgrad_grouped_workspace_floats", dtc(x0), g, n, oh, ow, cout, k, k,
+                       cin)) if split else 0
+    if nws:
+        ws = torch.empty((nws,), dtype=torch.float32, device=x0.device)
+        nv.call("cn_conv_wgrad_grouped_ws", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
+                ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil,
+                ctypes.addressof(dws), ws.data_ptr(), nws, nv.stream())
+    else:
+        nv.call("cn_conv_wgrad_grouped", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
+                ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil,
+                ctypes.addressof(dws), nv.stream())
     _prof_end(ev)
     return [dw for _, _, dw in jobs]
 

@@ -71,6 +71,17 @@ int cn_conv_wgrad_grouped(int dtype, int G, const void* const* xs, long long ldx
                           int Cin, const void* const* dys, long long lddy, int OH, int OW, int Cout,
                           int KH, int KW, int stride, int pad, int dil, float* const* dws,
                           hipStream_t stream);
+/* The same G problems split over K as well (small layer-1/2 shapes that fill the chip neither
+ * one by one nor grouped whole): one launch of G x nsplit K chunks into fp32 slabs ws[g][s][..],
+ * then one reduce launch summing each problem's slabs in split order into dws[g] (16-byte
+ * aligned).  ws: >= cn_conv_wgrad_grouped_workspace_floats(..) floats; 0 there, or a null /
+ * short ws, runs cn_conv_wgrad_grouped. */
+size_t cn_conv_wgrad_grouped_workspace_floats(int dtype, int G, int N, int OH, int OW, int Cout, int KH,
+                                              int KW, int Cin);
+int cn_conv_wgrad_grouped_ws(int dtype, int G, const void* const* xs, long long ldx, int N, int H,
+                             int W, int Cin, const void* const* dys, long long lddy, int OH, int OW,
+                             int Cout, int KH, int KW, int stride, int pad, int dil,
+                             float* const* dws, float* ws, size_t ws_floats, hipStream_t stream);
 /* out[i] (+)= sum_s ws[s*slab + i], s < nsplit  (split-K reduction, fp32) */
 int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                      int accumulate, hipStream_t stream);

@@ -155,6 +155,37 @@ def test_conv_wgrad_grouped(cuda, dt, case):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(4, 64, 30, 30, 128, 1, 1, 0, 1), (2, 32, 40, 40, 64, 3, 1, 1, 1),
+                                  (4, 128, 30, 30, 512, 1, 1, 0, 1), (2, 64, 36, 36, 64, 3, 1, 2, 2)])
+@pytest.mark.parametrize("G", [2, 4])
+def test_conv_wgrad_grouped_split(cuda, dt, case, G):
+    """The small-shape groups split over K as well (cn_conv_wgrad_grouped_ws: G x nsplit blocks
+    into per-problem slabs, one reduce launch): each problem against torch fp64; deterministic;
+    the shapes are chosen so the split path runs (workspace > 0)."""
+    n, cin, h, w, cout, k, s, p, d = case
+    oh, ow = ops.out_hw(h, w, k, s, p, d)
+    assert nv.query("cn_conv_wgrad_grouped_workspace_floats", ops.dtc(torch.empty(0, dtype=dt)), G, n,
+                    oh, ow, cout, k, k, cin) > 0
+    jobs, refs = [], []
+    for g in range(G):
+        x = rnd((n, cin, h, w), dt, 60 + g)
+        gy = rnd((n, cout, oh, ow), dt, 70 + g)
+        wr = torch.zeros((cout, cin, k, k), dtype=torch.float64, requires_grad=True)
+        F.conv2d(x, wr, None, s, p, d).backward(gy)
+        refs.append(wr.grad)
+        dw = torch.full((cout, k * k * cin), float("nan"), dtype=torch.float32, device=cuda)
+        jobs.append((nhwc(x).to(dt).to(cuda).contiguous(), nhwc(gy).to(dt).to(cuda).contiguous(), dw))
+    ops.conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d, split=True)
+    first = [dw.clone() for _, _, dw in jobs]
+    ops.conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d, split=True)
+    torch.cuda.synchronize()
+    wp = torch.empty((cout, cin, k, k), device=cuda).contiguous(memory_format=torch.channels_last)
+    for (_, _, dw), f, ref in zip(jobs, first, refs):
+        close(ops.as_param_grad(dw, wp), ref, dt)
+        assert torch.equal(dw, f)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 2), (2, 2)])
 def test_gemm_layouts_batched(cuda, dt, la, lb):
     B, M, N, K = 3, 77, 136, 200
