@@ -53,9 +53,10 @@ class GradSink(dict):
 # "end" (after the whole dgrad chain) or "layer" (after each layer's blocks: the queue's dY and
 # input tensors are released per layer).  CN_WGRAD_FLUSH selects it for A/B runs.
 WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
-# Small-shape groups split over K (cn_conv_wgrad_grouped_ws); CN_WGRAD_GSPLIT=0 issues them one
-# by one as split-K launches (A/B runs).
-WGRAD_GSPLIT = os.environ.get("CN_WGRAD_GSPLIT", "1") != "0"
+# Groups of >= 2 problems with fewer than CN_WGRAD_GSPLIT tiles (128x64 units) in total run split
+# over K as well (cn_conv_wgrad_grouped_ws); 0 issues the small ones one by one as split-K
+# launches (A/B runs).
+WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "128"))
 
 
 def _layer_index(enc):
@@ -94,13 +95,13 @@ class WgradQueue:
             tiles = -(-cout // 128) * -(-(k * k * cin) // 64)
             for i in range(0, len(jobs), ops.GROUP_MAX):
                 chunk = jobs[i:i + ops.GROUP_MAX]
-                if len(chunk) >= 3 and tiles * len(chunk) >= 128:
-                    ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
-                elif len(chunk) >= 2 and tiles * len(chunk) < 128 and WGRAD_GSPLIT:
+                if len(chunk) >= 2 and tiles * len(chunk) < WGRAD_GSPLIT:
                     # small shapes (layers 1-2): the group split over K as well -- one GEMM and
                     # one reduce launch instead of a split-K GEMM + reduce per problem
                     ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil,
                                            split=True)
+                elif len(chunk) >= 3 and tiles * len(chunk) >= 128:
+                    ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
                 else:
                     for x, dy, dw in chunk:
                         conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw)
