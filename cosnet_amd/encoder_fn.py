@@ -56,7 +56,7 @@ WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
 # Groups of >= 2 problems with fewer than CN_WGRAD_GSPLIT tiles (128x64 units) in total run split
 # over K as well (cn_conv_wgrad_grouped_ws); 0 issues the small ones one by one as split-K
 # launches (A/B runs).
-WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "128"))
+WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "512"))
 
 
 def _layer_index(enc):
