@@ -36,11 +36,6 @@ _SIGS = {
     "cn_conv_wgrad_grouped_workspace_floats": (_S, [_I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "cn_conv_wgrad_grouped_ws": (_I, [_I, _I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I,
                                       _I, _P, _P, _S, _P]),
-    "cn_conv_wgrad_slabs": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P,
-                                 _P]),
-    "cn_conv_wgrad_grouped_slabs": (_I, [_I, _I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I,
-                                         _I, _I, _P, _P, _S, _P]),
-    "cn_splitk_reduce_multi": (_I, [_I, _P, _P, _P, _P, _P]),
     "cn_splitk_reduce": (_I, [_P, _I, _L, _L, _P, _I, _P]),
     "cn_fp8_quant": (_I, [_I, _P, _L, _I, _I, _P, _L, _P, _I, _P]),
     "cn_fp8_quant_fmt": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _P, _I, _P]),

@@ -399,29 +399,10 @@ extern "C" size_t cn_conv_wgrad_workspace_floats(int dtype, int N, int OH, int O
   return ns > 1 ? (size_t)ns * Cout * KH * KW * Cin : 0;
 }
 
-static int wgrad_impl(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
-                      const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
-                      int stride, int pad, int dil, float* dw, float* ws, bool reduce, hipStream_t st);
-
 extern "C" int cn_conv_wgrad(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                              const void* dy, long long lddy, int OH, int OW, int Cout, int KH,
                              int KW, int stride, int pad, int dil, float* dw, float* ws,
                              hipStream_t st) {
-  return wgrad_impl(dtype, x, ldx, N, H, W, Cin, dy, lddy, OH, OW, Cout, KH, KW, stride, pad, dil, dw,
-                    ws, true, st);
-}
-
-extern "C" int cn_conv_wgrad_slabs(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
-                                   const void* dy, long long lddy, int OH, int OW, int Cout, int KH,
-                                   int KW, int stride, int pad, int dil, float* dw, float* ws,
-                                   hipStream_t st) {
-  return wgrad_impl(dtype, x, ldx, N, H, W, Cin, dy, lddy, OH, OW, Cout, KH, KW, stride, pad, dil, dw,
-                    ws, false, st);
-}
-
-static int wgrad_impl(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
-                      const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
-                      int stride, int pad, int dil, float* dw, float* ws, bool reduce, hipStream_t st) {
   if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
   GemmArgs a = gemm_defaults();
   a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
@@ -449,7 +430,7 @@ static int wgrad_impl(int dtype, const void* x, long long ldx, int N, int H, int
   a.c_mode = 3;
   a.slab = (long long)a.M * a.N;
   int rc = cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, 1, st);
-  if (rc || !reduce) return rc;
+  if (rc) return rc;
   return cn_splitk_reduce_impl(ws, ns, a.slab, a.slab, dw, 0, st);
 }
 
@@ -531,35 +512,11 @@ extern "C" size_t cn_conv_wgrad_grouped_workspace_floats(int dtype, int G, int N
   return ns > 1 ? (size_t)G * ns * Cout * KH * KW * Cin : 0;
 }
 
-static int wgrad_grouped_ws_impl(int dtype, int G, const void* const* xs, long long ldx, int N, int H,
-                                 int W, int Cin, const void* const* dys, long long lddy, int OH, int OW,
-                                 int Cout, int KH, int KW, int stride, int pad, int dil,
-                                 float* const* dws, float* ws, size_t ws_floats, bool reduce,
-                                 hipStream_t st);
-
 extern "C" int cn_conv_wgrad_grouped_ws(int dtype, int G, const void* const* xs, long long ldx, int N,
                                         int H, int W, int Cin, const void* const* dys, long long lddy,
                                         int OH, int OW, int Cout, int KH, int KW, int stride, int pad,
                                         int dil, float* const* dws, float* ws, size_t ws_floats,
                                         hipStream_t st) {
-  return wgrad_grouped_ws_impl(dtype, G, xs, ldx, N, H, W, Cin, dys, lddy, OH, OW, Cout, KH, KW, stride,
-                               pad, dil, dws, ws, ws_floats, true, st);
-}
-
-extern "C" int cn_conv_wgrad_grouped_slabs(int dtype, int G, const void* const* xs, long long ldx, int N,
-                                           int H, int W, int Cin, const void* const* dys, long long lddy,
-                                           int OH, int OW, int Cout, int KH, int KW, int stride, int pad,
-                                           int dil, float* const* dws, float* ws, size_t ws_floats,
-                                           hipStream_t st) {
-  return wgrad_grouped_ws_impl(dtype, G, xs, ldx, N, H, W, Cin, dys, lddy, OH, OW, Cout, KH, KW, stride,
-                               pad, dil, dws, ws, ws_floats, false, st);
-}
-
-static int wgrad_grouped_ws_impl(int dtype, int G, const void* const* xs, long long ldx, int N, int H,
-                                 int W, int Cin, const void* const* dys, long long lddy, int OH, int OW,
-                                 int Cout, int KH, int KW, int stride, int pad, int dil,
-                                 float* const* dws, float* ws, size_t ws_floats, bool reduce,
-                                 hipStream_t st) {
   if (G < 1 || G > GEMM_MAXG) return CN_ERR_SHAPE;
   if (Cin % vec_of(dtype) || Cout % vec_of(dtype)) return CN_ERR_ALIGN;
   int ns, ch, cfg;
@@ -594,7 +551,7 @@ static int wgrad_grouped_ws_impl(int dtype, int G, const void* const* xs, long l
   a.c_mode = 3;
   a.slab = slab;
   int rc = cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);
-  if (rc || !reduce) return rc;
+  if (rc) return rc;
   RedOut o;
   for (int g = 0; g < G; ++g) o.out[g] = dws[g];
   const long long n4 = slab / 4;
@@ -603,66 +560,6 @@ static int wgrad_grouped_ws_impl(int dtype, int G, const void* const* xs, long l
   hipLaunchKernelGGL(splitk_reduce_grouped_k, dim3((unsigned)bx, G), dim3(256), 0, st, (const float*)ws,
                      ns, slab, n4, o);
   CN_CHECK_LAUNCH();
-  return 0;
-}
-
-// ---- one reduce launch for many split-K weight gradients --------------------------------------
-// The weight gradients of an encoder backward's flush (encoder_fn.WgradQueue) that split over K
-// write their slabs only (cn_conv_wgrad_slabs / cn_conv_wgrad_grouped_slabs); this sums every
-// problem's slabs in split order into its dW -- one launch instead of one per problem.
-namespace {
-constexpr int MRED_MAX = 64;
-struct MultiRed {
-  const float* ws[MRED_MAX];
-  float* out[MRED_MAX];
-  long long n4[MRED_MAX];
-  long long slab[MRED_MAX];
-  int ns[MRED_MAX];
-};
-__global__ __launch_bounds__(256) void splitk_reduce_multi_k(MultiRed r) {
-  const int p = blockIdx.y;
-  const float* w = r.ws[p];
-  const long long n4 = r.n4[p], slab = r.slab[p];
-  const int nsplit = r.ns[p];
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    f32x4 a = {0.f, 0.f, 0.f, 0.f};
-    int s = 0;
-    for (; s + 8 <= nsplit; s += 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(w + (long long)(s + u) * slab + 4 * i);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) a += v[u];
-    }
-    for (; s < nsplit; ++s) a += *(const f32x4*)(w + (long long)s * slab + 4 * i);
-    ((f32x4*)r.out[p])[i] = a;
-  }
-}
-}  // namespace
-
-extern "C" int cn_splitk_reduce_multi(int n, const float* const* ws, const int* nsplit,
-                                      const long long* slab, float* const* out, hipStream_t st) {
-  for (int p0 = 0; p0 < n; p0 += MRED_MAX) {
-    const int m = n - p0 < MRED_MAX ? n - p0 : MRED_MAX;
-    MultiRed r = {};
-    long long most = 0;
-    for (int q = 0; q < m; ++q) {
-      const int p = p0 + q;
-      if (nsplit[p] < 1 || slab[p] % 4 || ((uintptr_t)ws[p] & 15) || ((uintptr_t)out[p] & 15))
-        return CN_ERR_ALIGN;
-      r.ws[q] = ws[p];
-      r.out[q] = out[p];
-      r.n4[q] = slab[p] / 4;
-      r.slab[q] = slab[p];
-      r.ns[q] = nsplit[p];
-      if (r.n4[q] > most) most = r.n4[q];
-    }
-    long long bx = (most + 255) / 256;
-    if (bx > 1024) bx = 1024;
-    if (bx < 1) bx = 1;
-    hipLaunchKernelGGL(splitk_reduce_multi_k, dim3((unsigned)bx, m), dim3(256), 0, st, r);
-    CN_CHECK_LAUNCH();
-  }
   return 0;
 }
 

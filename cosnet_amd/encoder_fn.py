@@ -57,7 +57,6 @@ WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
 # over K as well (cn_conv_wgrad_grouped_ws); 0 issues the small ones one by one as split-K
 # launches (A/B runs).
 WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "512"))
-WGRAD_MULTIRED = os.environ.get("CN_WGRAD_MULTIRED", "1") != "0"
 
 
 def _layer_index(enc):
@@ -88,9 +87,6 @@ class WgradQueue:
         return dw
 
     def flush(self):
-        # the K-split problems write slabs only; one reduce launch sums them all at the end
-        # (CN_WGRAD_MULTIRED=0: one reduce launch per problem / group, A/B runs)
-        defer = [] if WGRAD_MULTIRED else None
         for key, jobs in self.jobs.items():
             _, n, h, w, cin, _, oh, ow, cout, _, k, stride, pad, dil = key
             # grouped when >= 3 problems give >= 128 workgroups of 128x64 (two layer-4 1x1
@@ -103,14 +99,12 @@ class WgradQueue:
                     # small shapes (layers 1-2): the group split over K as well -- one GEMM and
                     # one reduce launch instead of a split-K GEMM + reduce per problem
                     ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil,
-                                           split=True, defer=defer)
+                                           split=True)
                 elif len(chunk) >= 3 and tiles * len(chunk) >= 128:
                     ops.conv_wgrad_grouped(chunk, n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
                 else:
                     for x, dy, dw in chunk:
-                        conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw,
-                                   defer=defer)
-        ops.reduce_deferred(defer)
+                        conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw)
         self.jobs = {}
 
 

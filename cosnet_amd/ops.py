@@ -337,10 +337,8 @@ def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accu
     return out
 
 
-def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None, defer=None):
-    """fp32 [cout, k*k*cin] weight gradient (channels_last order), fully overwritten.  defer (a
-    list): a K-split problem writes its slabs only and appends (ws, nsplit, slab, dw) for one
-    reduce_deferred() over many problems; dw is final only after that call."""
+def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
+    """fp32 [cout, k*k*cin] weight gradient (channels_last order), fully overwritten."""
     if dw is None:
         dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
     nws = int(nv.query("cn_conv_wgrad_workspace_floats", dtc(x), n, oh, ow, cout, k, k, cin))
@@ -348,37 +346,16 @@ def conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None, 
     es = x.element_size()
     ev = _prof_start(2.0 * n * oh * ow * cout * k * k * cin, ("wgrad", cout, k * k * cin, n * oh * ow),
                      es * (n * h * w * cin + n * oh * ow * cout) + 4 * cout * k * k * cin)
-    entry = "cn_conv_wgrad_slabs" if (defer is not None and nws) else "cn_conv_wgrad"
-    nv.call(entry, dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
+    nv.call("cn_conv_wgrad", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, dy.data_ptr(), ld(dy), oh,
             ow, cout, k, k, stride, pad, dil, dw.data_ptr(), nv.ptr(ws), nv.stream())
     _prof_end(ev)
-    if defer is not None and nws:
-        slab = cout * k * k * cin
-        defer.append((ws, 0, nws // slab, slab, dw))
     return dw
-
-
-def reduce_deferred(defer):
-    """The split-K sums of the weight gradients queued by conv_wgrad / conv_wgrad_grouped with
-    defer=: one cn_splitk_reduce_multi launch (per 64 problems), each problem's slabs in split
-    order."""
-    import ctypes
-    if not defer:
-        return
-    n = len(defer)
-    wsp = (ctypes.c_void_p * n)(*[ws.data_ptr() + 4 * off for ws, off, _, _, _ in defer])
-    nsp = (ctypes.c_int * n)(*[ns for _, _, ns, _, _ in defer])
-    slp = (ctypes.c_longlong * n)(*[slab for _, _, _, slab, _ in defer])
-    outp = (ctypes.c_void_p * n)(*[dw.data_ptr() for _, _, _, _, dw in defer])
-    nv.call("cn_splitk_reduce_multi", n, ctypes.addressof(wsp), ctypes.addressof(nsp),
-            ctypes.addressof(slp), ctypes.addressof(outp), nv.stream())
-    defer.clear()
 
 
 GROUP_MAX = 24       # cn_conv_wgrad_grouped's problem limit (gemm.h GEMM_MAXG)
 
 
-def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil, split=False, defer=None):
+def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil, split=False):
     """Weight gradients of G convs of ONE shape in one launch (cn_conv_wgrad_grouped): jobs =
     [(x, dy, dw)] with x [n*h*w, cin], dy [n*oh*ow, cout] sharing the row strides, dw fp32
     [cout, k*k*cin] (written).  No split-K workspace and no reduce launch.  split=True: the G
@@ -402,15 +379,9 @@ def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil, sp
                        cin)) if split else 0
     if nws:
         ws = torch.empty((nws,), dtype=torch.float32, device=x0.device)
-        nv.call("cn_conv_wgrad_grouped_slabs" if defer is not None else "cn_conv_wgrad_grouped_ws",
-                dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
+        nv.call("cn_conv_wgrad_grouped_ws", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
                 ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil,
                 ctypes.addressof(dws), ws.data_ptr(), nws, nv.stream())
-        if defer is not None:   # problem i's slabs: ws[i * ns * slab ..]
-            slab = cout * k * k * cin
-            ns = nws // (g * slab)
-            for i, (_, _, dw) in enumerate(jobs):
-                defer.append((ws, i * ns * slab, ns, slab, dw))
     else:
         nv.call("cn_conv_wgrad_grouped", dtc(x0), g, ctypes.addressof(xs), ld(x0), n, h, w, cin,
                 ctypes.addressof(dys), ld(dy0), oh, ow, cout, k, k, stride, pad, dil,

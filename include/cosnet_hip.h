@@ -82,21 +82,6 @@ int cn_conv_wgrad_grouped_ws(int dtype, int G, const void* const* xs, long long 
                              int W, int Cin, const void* const* dys, long long lddy, int OH, int OW,
                              int Cout, int KH, int KW, int stride, int pad, int dil,
                              float* const* dws, float* ws, size_t ws_floats, hipStream_t stream);
-/* cn_conv_wgrad / cn_conv_wgrad_grouped_ws without their reduce launch: when the problem splits
- * over K (workspace query > 0) only the fp32 slabs are written (ws[s][..], grouped: ws[g][s][..]),
- * for one cn_splitk_reduce_multi over a whole flush of weight gradients; otherwise dw / dws are
- * written directly, as the reducing entries do. */
-int cn_conv_wgrad_slabs(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
-                        const void* dy, long long lddy, int OH, int OW, int Cout, int KH, int KW,
-                        int stride, int pad, int dil, float* dw, float* ws, hipStream_t stream);
-int cn_conv_wgrad_grouped_slabs(int dtype, int G, const void* const* xs, long long ldx, int N, int H,
-                                int W, int Cin, const void* const* dys, long long lddy, int OH, int OW,
-                                int Cout, int KH, int KW, int stride, int pad, int dil,
-                                float* const* dws, float* ws, size_t ws_floats, hipStream_t stream);
-/* n split-K reductions in one launch: out[p][i] = sum_s ws[p][s*slab[p] + i], s < nsplit[p], in
- * split order (HOST arrays of n entries; 16-byte aligned buffers, slab[p] % 4 == 0). */
-int cn_splitk_reduce_multi(int n, const float* const* ws, const int* nsplit, const long long* slab,
-                           float* const* out, hipStream_t stream);
 /* out[i] (+)= sum_s ws[s*slab + i], s < nsplit  (split-K reduction, fp32) */
 int cn_splitk_reduce(const float* ws, int nsplit, long long slab, long long n, float* out,
                      int accumulate, hipStream_t stream);

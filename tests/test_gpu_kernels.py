@@ -186,51 +186,6 @@ def test_conv_wgrad_grouped_split(cuda, dt, case, G):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_wgrad_deferred_multi_reduce(cuda, dt):
-    """A flush's K-split weight gradients writing slabs only, summed by ONE cn_splitk_reduce_multi
-    launch (ops.reduce_deferred): grouped problems bitwise equal to their own reduce launch (same
-    split order), single problems within fp32 rounding of cn_conv_wgrad's grouped-order reduce,
-    and all against torch fp64."""
-    defer = []
-    singles, groups = [], []
-    # singles: a 3x3 and a 1x1 shape that split over K
-    for (n, cin, h, w, cout, k, s, p, d) in [(2, 64, 40, 40, 128, 3, 1, 1, 1), (4, 256, 30, 30, 64, 1, 1, 0, 1)]:
-        oh, ow = ops.out_hw(h, w, k, s, p, d)
-        assert nv.query("cn_conv_wgrad_workspace_floats", ops.dtc(torch.empty(0, dtype=dt)), n, oh, ow,
-                        cout, k, k, cin) > 0
-        x = rnd((n, cin, h, w), dt, 81)
-        gy = rnd((n, cout, oh, ow), dt, 82)
-        wr = torch.zeros((cout, cin, k, k), dtype=torch.float64, requires_grad=True)
-        F.conv2d(x, wr, None, s, p, d).backward(gy)
-        xg, gyg = nhwc(x).to(dt).to(cuda).contiguous(), nhwc(gy).to(dt).to(cuda).contiguous()
-        dw_ref = ops.conv_wgrad(xg, n, h, w, cin, gyg, oh, ow, cout, k, s, p, d)
-        dw = torch.full_like(dw_ref, float("nan"))
-        ops.conv_wgrad(xg, n, h, w, cin, gyg, oh, ow, cout, k, s, p, d, dw=dw, defer=defer)
-        singles.append((dw, dw_ref, wr.grad, (cout, cin, k)))
-    # a grouped split
-    n, cin, h, w, cout, k, s, p, d = (4, 64, 30, 30, 128, 1, 1, 0, 1)
-    oh, ow = ops.out_hw(h, w, k, s, p, d)
-    jobs, jobs_ref = [], []
-    for g in range(3):
-        x = nhwc(rnd((n, cin, h, w), dt, 90 + g)).to(dt).to(cuda).contiguous()
-        gy = nhwc(rnd((n, cout, oh, ow), dt, 95 + g)).to(dt).to(cuda).contiguous()
-        jobs.append((x, gy, torch.full((cout, k * k * cin), float("nan"), device=cuda)))
-        jobs_ref.append((x, gy, torch.empty((cout, k * k * cin), device=cuda)))
-    ops.conv_wgrad_grouped(jobs_ref, n, h, w, cin, oh, ow, cout, k, s, p, d, split=True)
-    ops.conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d, split=True, defer=defer)
-    assert len(defer) == 2 + 3
-    ops.reduce_deferred(defer)
-    torch.cuda.synchronize()
-    assert not defer
-    for (_, _, dw), (_, _, ref) in zip(jobs, jobs_ref):
-        assert torch.equal(dw, ref)
-    for dw, dw_ref, ref64, (cout, cin, k) in singles:
-        assert torch.allclose(dw, dw_ref, rtol=1e-5, atol=1e-5 * dw_ref.abs().max().item())
-        wp = torch.empty((cout, cin, k, k), device=cuda).contiguous(memory_format=torch.channels_last)
-        close(ops.as_param_grad(dw, wp), ref64, dt)
-
-
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 2), (2, 2)])
 def test_gemm_layouts_batched(cuda, dt, la, lb):
     B, M, N, K = 3, 77, 136, 200
