@@ -11,6 +11,8 @@ Semantics kept from the reference: labels come from frame b (:146); cat order [Z
 constants (:178-182); the whole depth b-side head is no_grad (:240-247); BN running stats
 update on both a- and b-side calls in train mode.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -57,7 +59,8 @@ class RGBDSegmentation_RAA(nn.Module):
         self.compute_dtype = torch.bfloat16
         self.fp8 = None            # Fp8Context: e4m3 forward conv GEMMs in the encoders (configs[4])
         self.pair_encoder = True   # batch frames a and b through each encoder (encoder_fn.py)
-        self.concurrent_encoders = True   # depth encoder on a second stream (forward())
+        # depth encoder on a second stream (forward()); CN_CONCURRENT_ENCODERS=0 for A/B runs
+        self.concurrent_encoders = os.environ.get("CN_CONCURRENT_ENCODERS", "1") != "0"
         self._to_channels_last()
         self.register_state_dict_pre_hook(_flush_bn_counters)
 
