@@ -41,8 +41,17 @@ class TrainStep:
     """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
 
     def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None,
-                 grad_dtype="fp32"):
+                 grad_dtype="fp32", split_graphs=None):
         self.model, self.opt = model, opt
+        # split_graphs (single process, encoders on two streams): record the step as one-stream
+        # graphs per phase and stream instead of one graph with a forked branch (_split_capture).
+        # ROCm's launch of a multi-stream graph blocks the host for ~the replay's duration, so
+        # the device starts every step behind a host still submitting it; one-stream graphs
+        # return at once (tools/probes/graph_fork_probe.py, profiles/r04_graph_replay_host_probe.txt).
+        if split_graphs is None:
+            split_graphs = os.environ.get("CN_SPLIT_GRAPHS", "0") == "1"
+        self.split_graphs = bool(split_graphs)
+        self._split = None
         self.grad_dtype = grad_dtype
         self.l1 = float(l1_weight)
         self.graphed = graphed
@@ -119,6 +128,87 @@ class TrainStep:
         self._mem(" After backward")
         self.loss = loss.detach()
         self.opt.step()
+
+    # ---- split recording: one-stream graphs per phase and stream -------------------------------
+    def _split_ok(self):
+        m = self.model
+        return (self.split_graphs and self.world == 1 and self.stream is not None
+                and getattr(m, "pair_encoder", False) and getattr(m, "no_grad_for_counterpart", False)
+                and m._side_stream(self.rgb_a.device) is not None
+                and self.rgb_a.shape == self.rgb_b.shape)
+
+    def _split_capture(self, s1):
+        """The step as six one-stream graphs, the model's forward / backward cut at its four
+        cross-stream edges (rgbd_segmentation_RAA.forward: depth encoder + depth head on the side
+        stream, joined before the decoder; autograd runs their backward there too):
+            s1: A  RGB encoder + RGB head       s2: A' depth encoder + depth head
+            s1: B  decoder + loss + their backward (gradients of the three head outputs)
+            s1: C  RGB head + encoder backward  s2: C' depth head + encoder backward
+            s1: D  SGD
+        Each stream's graphs draw on a pool of their own: a graph of one stream never reuses
+        memory a concurrently running graph of the other stream still holds.  The kernels and
+        their order per stream are those of the one-graph recording (bitwise-equal results,
+        tests/test_gpu_train_step.py)."""
+        from .encoder_fn import encode_pair
+        m = self.model
+        s2 = m._side_stream(self.rgb_a.device)
+        p1, p2 = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+        isz = tuple(self.rgb_a.shape[2:])
+        self.opt.zero_grad()
+        m._set_dtype()
+        s2.wait_stream(s1)
+        gA, hA, gB, gC, hC, gD = (torch.cuda.CUDAGraph() for _ in range(6))
+        with torch.cuda.graph(gA, stream=s1, pool=p1):
+            va, vb, geo = encode_pair(m.encoder, self.rgb_a, self.rgb_b)
+            with torch.no_grad():
+                m.encoder.annotate_nhwc(vb, geo, isz)                      # labels (:146)
+            z_a, z_b = m._rgb_head(va, vb, geo)
+        with torch.cuda.graph(hA, stream=s2, pool=p2):
+            da, db, dgeo = encode_pair(m.depth_encoder, self.dep_a, self.dep_b)
+            dz_a, dz_b = m._depth_head(da, db, dgeo)
+        if dgeo != geo:
+            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+        outs = [t for t in (z_a, z_b, dz_a) if t.requires_grad]
+        dec = [p for mod in (m.segmentation_classifier_A, m.segmentation_classifier_B)
+               for p in mod.parameters() if p.requires_grad]
+        with torch.cuda.graph(gB, stream=s1, pool=p1):
+            x1, x2 = m._decode(z_a, z_b, dz_a, dz_b, geo, isz)
+            loss = fn.BceL1PairDevFn.apply(x1, x2, self.gt_a, self.gt_b, self.cnt, self.total, self.l1)
+            grads = torch.autograd.grad(loss, outs + dec, self._one)
+            for p, g in zip(dec, grads[len(outs):]):
+                p.grad = g
+        gout = dict(zip([id(t) for t in outs], grads[:len(outs)]))
+        rgb = [(t, gout[id(t)]) for t in (z_a, z_b) if id(t) in gout]
+        with torch.cuda.graph(gC, stream=s1, pool=p1):
+            torch.autograd.backward([t for t, _ in rgb], [g for _, g in rgb])
+        with torch.cuda.graph(hC, stream=s2, pool=p2):
+            if id(dz_a) in gout:
+                torch.autograd.backward([dz_a], [gout[id(dz_a)]])
+        with torch.cuda.graph(gD, stream=s1, pool=p1):
+            self.opt.step()
+        self.loss = loss.detach()
+        # the graphs read these across their boundaries: keep them (and their memory) alive
+        self._split = {"s2": s2, "g": (gA, hA, gB, gC, hC, gD),
+                       "keep": (va, vb, z_a, z_b, da, db, dz_a, dz_b, x1, x2, grads)}
+        self.graph = gA
+
+    def _split_replay(self):
+        sp = self._split
+        s2 = sp["s2"]
+        gA, hA, gB, gC, hC, gD = sp["g"]
+        cur = torch.cuda.current_stream()
+        s2.wait_stream(cur)              # inputs, counts and learning rates of this step
+        with torch.cuda.stream(s2):
+            hA.replay()
+        gA.replay()
+        cur.wait_stream(s2)
+        gB.replay()
+        s2.wait_stream(cur)
+        with torch.cuda.stream(s2):
+            hC.replay()
+        gC.replay()
+        cur.wait_stream(s2)
+        gD.replay()
 
     # ---- data parallel: arena, buckets, deferred encoder backward ----------------------------
     def _bind(self):
@@ -298,6 +388,8 @@ class TrainStep:
         try:
             if self.world > 1:
                 self._dp_capture(s)
+            elif self._split_ok():
+                self._split_capture(s)
             else:
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph, stream=s):
@@ -396,6 +488,8 @@ class TrainStep:
         self._counts()
         if self.world > 1:
             self._dp_replay()
+        elif self._split is not None:
+            self._split_replay()
         else:
             self.graph.replay()
         self.loss = self._graph_loss

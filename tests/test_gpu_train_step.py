@@ -9,7 +9,7 @@ from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
 from cosnet_amd.train_step import TrainStep
 
 
-def _setup(cuda, dtype, graphed, b=2, s=65):
+def _setup(cuda, dtype, graphed, b=2, s=65, split=False):
     torch.manual_seed(0)
     m = C.build_model(dtype)
     m.load_state_dict(recipe_state_dict(m.state_dict()))
@@ -17,7 +17,7 @@ def _setup(cuda, dtype, graphed, b=2, s=65):
     m = m.to(cuda).train()
     g0, g1 = reference_param_groups(m)
     opt = SGD([g0, g1], [0.0, 0.0])
-    st = TrainStep(m, opt, b, s, graphed=graphed)
+    st = TrainStep(m, opt, b, s, graphed=graphed, split_graphs=split)
     st.load(*[t.to(cuda) for t in synthetic_inputs(b, s, s, seed=5)])
     return m, st
 
@@ -32,17 +32,20 @@ def _bufs(st):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_graph_step_matches_eager(cuda, dtype):
+def test_graph_step_matches_eager(cuda, dtype, split):
     """Graph replays follow the eager trajectory BIT FOR BIT: every reduction of the step is a
     fixed-order sum (no float atomics, no memset nodes), so two eager runs are bitwise
     identical, and so is the replayed graph -- losses, every SGD momentum buffer (the running
     sum of each parameter's gradients, so a gradient contribution missing from the recording
-    shows up) and the BN running statistics."""
-    runs = [_setup(cuda, dtype, graphed=g) for g in (False, False, True)]
+    shows up) and the BN running statistics.  split: the step recorded as one-stream graphs per
+    phase and stream (TrainStep split_graphs)."""
+    runs = [_setup(cuda, dtype, graphed=g, split=split and g) for g in (False, False, True)]
     for _, st in runs:
         st.opt.set_lrs(_lrs(0))
         st.capture(warmup=2)
+    assert (runs[2][1]._split is not None) == split
     losses = [[], [], []]
     for i in range(2):
         for r, (_, st) in enumerate(runs):
