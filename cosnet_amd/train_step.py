@@ -29,6 +29,8 @@ BN running statistics stay per rank during training (train-mode BN normalises wi
 statistics, so they never enter the step); sync_buffers() broadcasts rank 0's before evaluation
 or checkpointing.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
