@@ -47,11 +47,12 @@ class TrainStep:
         self.model, self.opt = model, opt
         # split_graphs (single process, encoders on two streams): record the step as one-stream
         # graphs per phase and stream instead of one graph with a forked branch (_split_capture).
-        # ROCm's launch of a multi-stream graph blocks the host for ~the replay's duration, so
-        # the device starts every step behind a host still submitting it; one-stream graphs
-        # return at once (tools/probes/graph_fork_probe.py, profiles/r04_graph_replay_host_probe.txt).
+        # ROCm's launch of a multi-stream graph blocks the host for ~the replay's duration; the
+        # one-stream graphs return at once (0.8 ms per step), so the host's own work between
+        # steps (the loader's decode / augmentation in train.py) overlaps the device's step.  The
+        # device time per step is the same either way (profiles/r04_split_graphs_ab.txt).
         if split_graphs is None:
-            split_graphs = os.environ.get("CN_SPLIT_GRAPHS", "0") == "1"
+            split_graphs = os.environ.get("CN_SPLIT_GRAPHS", "1") == "1"
         self.split_graphs = bool(split_graphs)
         self._split = None
         self.grad_dtype = grad_dtype
