@@ -629,7 +629,7 @@ template <class T> int grid_rows(int P, int C, int* gx, int min_rows, int blocks
   return gy < 1 ? 1 : gy;
 }
 
-int g_tune[8] = {1024, SUNR, 2048, UNR, 1024, UNR, 2048, UNR};  // see cn_bn_set_tuning
+int g_tune[8] = {1024, SUNR, 2048, UNR, 512, UNR, 2048, UNR};  // see cn_bn_set_tuning; bwd-reduce 512: profiles/r04_bn_tune_ab.txt
 enum { T_ST_BLOCKS, T_ST_ROWS, T_AP_BLOCKS, T_AP_ROWS, T_BR_BLOCKS, T_BR_ROWS, T_BA_BLOCKS, T_BA_ROWS };
 
 template <class T> int stat_splits(int P, int C, int nseg, int* gx) {
