@@ -25,32 +25,58 @@ sys.path.insert(0, REPO)
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E (MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(REPO, "profiles", "r04_pmc_step_traffic.json")
-ROCPROF_FILE = os.path.join(REPO, "profiles", "r04_rocprof_kernel_stats_bench_b4_473.csv")
+# Index of the committed profiles the line cross-checks its live numbers against, with the source
+# hash of the library they were taken with (tools/profile_index.py writes it after a profiling pass)
+PROFILE_INDEX = os.path.join(REPO, "profiles", "current.json")
+
+
+def committed_profile(kind):
+    """(path, provenance) of the committed profile `kind` ("rocprof_stats", "coatt_trace", "pmc"):
+    provenance = {"lib_source_hash" of the profiled library, "stale": whether the library loaded
+    now was built from other sources -- then the committed numbers describe older kernels}."""
+    try:
+        with open(PROFILE_INDEX) as f:
+            idx = json.load(f)
+        path = os.path.join(REPO, idx[kind])
+    except (OSError, KeyError, ValueError):
+        return None, None
+    try:
+        from cosnet_amd import _native as nv
+        now = nv.load().cn_build_source_hash().decode()
+    except Exception:
+        now = None
+    return path, {"profiled_lib_source_hash": idx.get("lib_source_hash"), "loaded_lib_source_hash": now,
+                  "stale": now != idx.get("lib_source_hash")}
 
 
 def rocprof_avg_us(substr):
     """Average launch duration of a kernel family in the committed rocprofv3 --stats summary of
     this same bench command (the cross-check of the live HIP-event timing)."""
+    path, prov = committed_profile("rocprof_stats")
+    if path is None:
+        return None
     try:
         import csv
-        with open(ROCPROF_FILE) as f:
+        with open(path) as f:
             rows = [r for r in csv.DictReader(f) if substr in r["Name"]]
         n = sum(int(r["Calls"]) for r in rows)
-        return {"avg_launch_us": sum(float(r["TotalDurationNs"]) for r in rows) / n / 1e3,
-                "launches": n, "source": os.path.relpath(ROCPROF_FILE, REPO)} if n else None
+        return dict({"avg_launch_us": sum(float(r["TotalDurationNs"]) for r in rows) / n / 1e3,
+                     "launches": n, "source": os.path.relpath(path, REPO)}, **prov) if n else None
     except (OSError, KeyError, ValueError):
         return None
-COATT_TRACE_FILE = os.path.join(REPO, "profiles", "r04_coatt_trace.json")
 
 
 def coatt_trace():
     """Co-attention kernel time per training step / per configs[3] launch from the committed
     rocprofv3 --kernel-trace summary of this bench command (tools/coatt_trace_summary.py)."""
+    path, prov = committed_profile("coatt_trace")
+    if path is None:
+        return None
     try:
-        with open(COATT_TRACE_FILE) as f:
+        with open(path) as f:
             d = json.load(f)
-        d["source"] = os.path.relpath(COATT_TRACE_FILE, REPO) + ": " + d.get("source", "")
+        d["source"] = os.path.relpath(path, REPO) + ": " + d.get("source", "")
+        d.update(prov)
         return d
     except (OSError, ValueError):
         return None
@@ -90,11 +116,15 @@ def parse():
 def pmc_traffic(family):
     """HBM traffic per launch of a kernel family from the committed rocprofv3 PMC summary
     (tools/pmc_run.sh + tools/pmc_summary.py over this bench's own eager step)."""
+    path, prov = committed_profile("pmc")
+    if path is None:
+        return None
     try:
-        with open(PMC_FILE) as f:
+        with open(path) as f:
             d = json.load(f)
         e = dict(d["families"][family])
-        e["source"] = os.path.relpath(PMC_FILE, REPO) + ": " + d["source"]
+        e["source"] = os.path.relpath(path, REPO) + ": " + d["source"]
+        e.update(prov)
         return e
     except (OSError, KeyError, ValueError):
         return None
@@ -444,6 +474,7 @@ def main():
                            "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
                            "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
                            "traffic_source": pmc["source"] if pmc else None,
+                           "traffic_stale": pmc["stale"] if pmc else None,
                            "algorithmic_bytes_per_launch": nbytes / n,
                            "event_avg_launch_us": kt / n * 1e6,
                            "rocprof": rocprof_avg_us("gemm_kernel"),
@@ -475,7 +506,8 @@ def main():
             if tr:
                 us = tr["train_us_per_step"]
                 out["roofline_coattention_train"]["rocprof"] = {
-                    "us_per_step": us, "frac": ffl / sc / (us * 1e-6) / 1e12 / peak, "source": tr["source"]}
+                    "us_per_step": us, "frac": ffl / sc / (us * 1e-6) / 1e12 / peak, "source": tr["source"],
+                    "stale": tr["stale"]}
     log("timed: %.1f ms/step" % (dt / args.steps * 1e3))
     if prof and dtype == torch.bfloat16 and S == 473:
         out["roofline_coattention"] = rc = coattention_roofline(dev)
@@ -484,7 +516,7 @@ def main():
             us = tr["configs3_us_per_launch"]
             alg = rc["achieved"] * rc["us_per_launch"] * 1e-6 * 1e12
             rc["rocprof"] = {"us_per_launch": us, "frac": alg / (us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-                             "source": tr["source"]}
+                             "source": tr["source"], "stale": tr["stale"]}
     if args.fp32_extra and dtype == torch.bfloat16 and world == 1 and not args.no_roofline:
         log("fp32 extra ...")
         out["fp32_extra"] = extra_line(dev, B, S, "fp32")

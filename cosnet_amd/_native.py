@@ -112,6 +112,7 @@ _SIGS = {
     "cn_colsum": (_I, [_I, _P, _L, _I, _I, _P, _P, _P]),
     "cn_cast2d": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _I, _P]),
     "cn_build_source_hash": (ctypes.c_char_p, []),
+    "cn_build_experimental": (_I, []),
 }
 
 _lib = None
@@ -138,7 +139,7 @@ def load():
 
 
 HASHED_SOURCES = ["gemm.hip", "conv.hip", "bn.hip", "ew.hip", "coatt.hip", "coatt_fused.hip",
-                  "coatt_dsplit.hip", "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip",
+                  "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip",
                   "common.h", "gemm.h", "coatt_fused.h", "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
 
 

@@ -392,6 +392,9 @@ void coatt_fused_fwd_k(FusedArgs a) {
   }
 }
 
+#if CN_EXPERIMENTAL
+// Measured-slower wave-pair variants (round 4): built only with CN_EXPERIMENTAL=1
+// (make EXPERIMENTAL=1), selected by cn_coatt_force_variant / CN_COATT_VARIANT in such builds.
 // ---------------------------------------------------------------------------------------------
 // Two waves per SIMD (coatt_fused2_k): the same flash product, 8 waves = 4 wave PAIRS per
 // workgroup, 128 query rows.  Both waves of a pair hold the pair's 32 query rows in registers (Q,
@@ -953,6 +956,7 @@ void coatt_fused3_k(FusedArgs a) {
       }
   }
 }
+#endif  // CN_EXPERIMENTAL
 
 // Fold the key-split partials of one row of a tail item: O = sum_s 2^(m_s - M) O_s /
 // sum_s 2^(m_s - M) l_s, splits in order (deterministic).  One thread = 8 channels of one row.
@@ -1041,14 +1045,16 @@ static int coatt_variant() {
   static const int v = [] {
     const char* e = getenv("CN_COATT_VARIANT");
     const int x = e ? atoi(e) : 1;
-    return (x >= 1 && x <= 4) ? x : 1;
+    return (x >= 1 && x <= (CN_EXPERIMENTAL ? 4 : 1)) ? x : 1;
   }();
   return g_coatt_variant ? g_coatt_variant : v;
 }
 
 // Development / test hook: force the forward / PV kernel variant (1..4 as above; 0: default).
 // Returns the previous setting.
+// Variants 2-4 exist only in CN_EXPERIMENTAL builds (-1 otherwise, nothing changed).
 extern "C" int cn_coatt_force_variant(int v) {
+  if (!CN_EXPERIMENTAL && v >= 2 && v <= 4) return -1;
   const int old = g_coatt_variant;
   g_coatt_variant = (v >= 1 && v <= 4) ? v : 0;
   return old;
@@ -1065,6 +1071,7 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   a.nwork = nfull8 + (a.nitems - a.nfull) * a.nsplit;
   dim3 grid(a.nwork);
   const int var = coatt_variant();
+#if CN_EXPERIMENTAL
   if (var == 2) {
     if (mode == 0) hipLaunchKernelGGL(coatt_fused2_k<0>, grid, dim3(F2NT), 0, st, a);
     else hipLaunchKernelGGL(coatt_fused2_k<1>, grid, dim3(F2NT), 0, st, a);
@@ -1074,7 +1081,10 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
   } else if (var == 4) {
     const int rc = coatt_dsplit_launch(mode, a, grid, st);
     if (rc) return rc;
-  } else {
+  } else
+#endif
+  {
+    (void)var;
     if (mode == 0) hipLaunchKernelGGL(coatt_fused_fwd_k<0>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(coatt_fused_fwd_k<1>, grid, dim3(256), 0, st, a);
   }

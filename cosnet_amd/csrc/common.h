@@ -15,6 +15,13 @@ typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// Measured-and-rejected kernel variants (co-attention wave pairs, GEMM tile configurations 21-25)
+// are compiled only into development builds (make EXPERIMENTAL=1); the product library keeps the
+// code that runs by default.
+#ifndef CN_EXPERIMENTAL
+#define CN_EXPERIMENTAL 0
+#endif
+
 // dtype codes shared with the C ABI (include/cosnet_hip.h)
 enum { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2, DT_FP8_E5M2 = 3 };  // DT_FP8_E5M2 GEMM: A e5m2, B e4m3
 

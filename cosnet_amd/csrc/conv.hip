@@ -378,7 +378,8 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
     }
   } else {
     *cfg = -1;
-    tiles = (long long)((M + 127) / 128) * ((NN + 63) / 64);
+    // the fp32 parity path's 128x64 tiles; a group's G problems share the block target
+    tiles = (long long)((M + 127) / 128) * ((NN + 63) / 64) * G;
   }
   long long want = (target + tiles - 1) / tiles;
   long long maxs = K / (8 * BK);

@@ -970,7 +970,7 @@ static int heuristic_cfg(int M, int N, int K, int bz) {
   // Round 4: 128x128 / 8 waves for these products (layer-3 3x3 fwd 38 vs 46 us, 1x1 fwd 22 vs 25
   // us isolated; whole step +0.2 %: profiles/r04_gemm_n256_tiles_ab.txt).  CN_GEMM_N256 overrides
   // it for A/B runs (19 = the round-3 128x256 ping-pong, 24 / 25 = K-split wave groups).
-  static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); return e ? atoi(e) : 11; }();
+  static const int n256 = [] { const char* e = getenv("CN_GEMM_N256"); const int v = e ? atoi(e) : 11; return (v >= 21 && !CN_EXPERIMENTAL) ? 11 : v; }();
   if (N == 256 && K >= 1024 && tiles_of(19, M, N) * bz >= 200) return n256;
   // shallow wide products (1x1 convs with K <= 512 into >= 1024 channels): 256x256 by the
   // round-3 isolated sweep; CN_GEMM_SHALLOW overrides it for in-step A/B runs
@@ -1011,10 +1011,12 @@ static int launch_epi(const GemmArgs& a, hipStream_t st) {
       case 18: return launch_c<T, T, 18, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 19: return launch_c<T, T, 19, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 20: return launch_c<T, T, 20, LA, L_KC_DENSE, EPI>(a, 1, st);
+#if CN_EXPERIMENTAL
       case 21: return launch_c<T, T, 21, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 22: return launch_c<T, T, 22, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 24: return launch_c<T, T, 24, LA, L_KC_DENSE, EPI>(a, 1, st);
       case 25: return launch_c<T, T, 25, LA, L_KC_DENSE, EPI>(a, 1, st);
+#endif
       default: return CN_ERR_UNSUPPORTED;
     }
   }
@@ -1044,6 +1046,7 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
       case 15: return launch_c<T, CT, 15, LA, LB>(a, batch, st);
       case 16: return launch_c<T, CT, 16, LA, LB>(a, batch, st);
       case 17: return launch_c<T, CT, 17, LA, LB>(a, batch, st);
+#if CN_EXPERIMENTAL
       case 21: return launch_c<T, CT, 21, LA, LB>(a, batch, st);
       case 22: return launch_c<T, CT, 22, LA, LB>(a, batch, st);
       case 23: return launch_c<T, CT, 10, LA, LB>(a, batch, st);   // 4 waves of 128x128 spill: not built
@@ -1056,6 +1059,7 @@ static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
           return launch_c<T, CT, 11, LA, LB>(a, batch, st);
         }
       }
+#endif
       case 18: case 19: case 20: {  // ping-pong tiles: k-contiguous operands only
         constexpr bool kc = LA != L_MC_DENSE && LA != L_MC_CONV && LB != L_MC_DENSE && LB != L_MC_CONV;
         if constexpr (kc) {
@@ -1189,7 +1193,7 @@ long long cn_gemm_cfg_blocks(int cfg, int M, int N) {
 
 // Development hook: force one tile configuration for every bf16 launch (-1 = heuristic).
 extern "C" int cn_gemm_force_config(int cfg) {
-  if (cfg >= kNumCfg) return -1;
+  if (cfg >= kNumCfg || (!CN_EXPERIMENTAL && cfg >= 21)) return -1;
   g_force_cfg = cfg;
   return kNumCfg;
 }

@@ -567,7 +567,14 @@ class ShapeGraphCache:
                            grad_dtype=self.grad_dtype)
             st.load(*ins)
             self.opt.set_lrs(lrs)
-            st.capture(warmup=1)          # this batch's step runs eagerly, then the record
+            try:
+                st.capture(warmup=1)      # this batch's step runs eagerly, then the record
+            except BaseException:
+                # admit() reserved the slot: a failed recording (OOM, capture error) must not
+                # leave a placeholder that the next batch of this size would "hit"
+                self.graphs.pop(hw, None)
+                self.evicted.add(hw)
+                raise
             self.graphs[hw] = st
             return st.loss
         if self.eager is None:

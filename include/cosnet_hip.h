@@ -381,9 +381,13 @@ int cn_frame_resize(int src_u8, const void* src, int C, long long plane_stride, 
 /* Build provenance: SHA-256 (16 hex digits) of the HIP sources + this header the library was
  * compiled from (stamped by csrc/Makefile). */
 const char* cn_build_source_hash(void);
+/* 1 if the library was built with the development variants (make EXPERIMENTAL=1: co-attention
+ * kernel variants 2-4, GEMM tile configurations 21-25), else 0. */
+int cn_build_experimental(void);
 
 /* Development hook (tuning tools only): force GEMM tile configuration `cfg` for every bf16
- * launch; -1 restores the shape heuristic.  Returns the number of configurations. */
+ * launch; -1 restores the shape heuristic.  Returns the number of configurations, or -1 for a
+ * configuration this build does not carry (21-25 without EXPERIMENTAL=1). */
 int cn_gemm_force_config(int cfg);
 /* Development hook (tuning tools only): number of blocks the wgrad K split aims for. */
 int cn_gemm_set_wgrad_target(int blocks);
@@ -391,7 +395,8 @@ int cn_gemm_set_wgrad_target(int blocks);
  * per SIMD; 2: eight waves in pairs that split the output channels, S computed by both; 3: pairs
  * that split the keys of S and the output channels; 4: four waves in pairs of 64 query rows that
  * split the channels of S (partial S exchanged through LDS) and of the output; 0: default).
- * Returns the previous setting.  CN_COATT_VARIANT sets the default. */
+ * Returns the previous setting, or -1 for variants 2-4 in a library built without them
+ * (cn_build_experimental() == 0).  CN_COATT_VARIANT sets the default. */
 int cn_coatt_force_variant(int v);
 
 #ifdef __cplusplus

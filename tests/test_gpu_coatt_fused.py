@@ -162,6 +162,14 @@ def test_flash_training_fwd_bwd_vs_fp64(cuda, n, hw, which):
         assert e <= 3e-2, (name, e)
 
 
+def _need_variants(lib):
+    """Variants 2-4 were measured slower and live only in the development library
+    (make EXPERIMENTAL=1, loaded through COSNET_HIP_LIB); the product library refuses them."""
+    if not lib.cn_build_experimental():
+        assert lib.cn_coatt_force_variant(2) == -1
+        pytest.skip("co-attention variants 2-4 are built only with EXPERIMENTAL=1")
+
+
 @pytest.mark.parametrize("n,hw", [(1, 97), (2, 169), (1, 1271), (4, 3600), (5, 3600)])
 def test_paired_wave_kernel_is_bitwise_the_four_wave_kernel(cuda, n, hw):
     """The 8-wave forward (coatt_fused2_k: wave pairs share 32 query rows and split the output
@@ -169,6 +177,7 @@ def test_paired_wave_kernel_is_bitwise_the_four_wave_kernel(cuda, n, hw):
     MFMA sequence as the 4-wave kernel: no-grad forward (incl. the key-split tail), training
     forward (LSE) and the PV backward kernel (per-key normaliser, accumulate) are bitwise equal."""
     lib = nv.load()
+    _need_variants(lib)
     vat, va, vb = make(n, hw, 256, cuda, seed=hw + 7, scale=0.8)
     g = torch.Generator().manual_seed(n * hw)
     dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)
@@ -209,6 +218,7 @@ def test_split_pair_kernels(cuda, n, hw, var):
     forward's LSE to 1e-4 (only S's summation order differs) and the PV backward kernel within
     the bf16 output rounding."""
     lib = nv.load()
+    _need_variants(lib)
     vat, va, vb = make(n, hw, 256, cuda, seed=hw + 11, scale=0.8)
     g = torch.Generator().manual_seed(n * hw + 1)
     dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)

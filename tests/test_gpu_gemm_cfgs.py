@@ -20,9 +20,16 @@ CFGS = [11, 13, 10, 15, 4, 18, 19, 20, 21, 22, 23, 24, 25]
 EPI_CFGS = {10, 11, 12, 13, 18, 19, 20, 21, 22, 24, 25}   # the tiles launch_epi instantiates
 
 
+EXPERIMENTAL_CFGS = {21, 22, 23, 24, 25}   # development builds only (make EXPERIMENTAL=1)
+
+
 @pytest.fixture
-def force_cfg():
+def force_cfg(request):
     lib = nv.load()
+    cfg = request.node.callspec.params.get("cfg") if hasattr(request.node, "callspec") else None
+    if cfg in EXPERIMENTAL_CFGS and not lib.cn_build_experimental():
+        assert lib.cn_gemm_force_config(cfg) == -1   # the product library refuses it
+        pytest.skip("tile configuration %d is built only with EXPERIMENTAL=1 (COSNET_HIP_LIB)" % cfg)
     yield lib.cn_gemm_force_config
     lib.cn_gemm_force_config(-1)
 

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 PMC passes into per-kernel-family HBM traffic per launch.
 
-    python tools/pmc_summary.py FETCH_DIR WRITE_DIR [MFMA_DIR] > profiles/r01_pmc_gemm.json
+    python tools/pmc_summary.py [--steps 2] FETCH_DIR WRITE_DIR [MFMA_DIR] > profiles/rNN_pmc_step_traffic.json
 
 Each *_DIR holds the `*_counter_collection.csv` of ONE `rocprofv3 --pmc` pass over the same
 command (`python bench.py --graph 0 --steps 1 --warmup 1 --cpu-baseline 0 --no-roofline`):
@@ -45,9 +45,17 @@ def load(d):
 
 
 def main():
-    fetch = load(sys.argv[1])
-    write = load(sys.argv[2])
-    mfma = load(sys.argv[3]) if len(sys.argv) > 3 else {}
+    args = sys.argv[1:]
+    # the profiled command runs --warmup 1 + --steps 1 eager steps = TWO steps (816 GEMM
+    # launches = 2 x 408): per-step totals divide by this
+    steps = 2
+    if "--steps" in args:
+        i = args.index("--steps")
+        steps = int(args[i + 1])
+        del args[i:i + 2]
+    fetch = load(args[0])
+    write = load(args[1])
+    mfma = load(args[2]) if len(args) > 2 else {}
     fam = defaultdict(lambda: defaultdict(float))
     for did, (name, cs) in fetch.items():
         f = fam[family(name)]
@@ -77,9 +85,12 @@ def main():
                 e[c] = f[c]
         res[k] = e
     tot = sum(e["traffic_bytes_total"] for e in res.values())
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, one eager train step "
-                     "(bench.py --graph 0 --steps 1 --warmup 1), gfx950 FETCH_SIZE x2 correction",
-           "step_traffic_bytes": tot,
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over %d eager train steps "
+                     "(bench.py --graph 0 --steps 1 --warmup 1: one warm-up + one timed step), gfx950 "
+                     "FETCH_SIZE x2 correction" % steps,
+           "profiled_steps": steps,
+           "profiled_traffic_bytes": tot,
+           "step_traffic_bytes": tot / steps,
            "families": dict(sorted(res.items(), key=lambda kv: -kv[1]["traffic_bytes_total"]))}
     json.dump(out, sys.stdout, indent=1)
     print()

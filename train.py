@@ -304,6 +304,17 @@ def main(argv=None):
     t_start = time.time()
     loss_history = []
     captured = False
+    pending = None
+
+    def report(ep, it, lt, lr):
+        lv = float(lt.item()) / world
+        loss_history.append(lv)
+        say("===> Epoch[{}]({}/{}): Loss: {:.10f}  lr: {:.5f}".format(ep, it, train_len, lv, lr))
+        if logger:
+            logger.write("Epoch[{}]({}/{}):     Loss: {:.10f}      lr: {:.5f}\n".format(
+                ep, it, train_len, lv, lr))
+            logger.flush()
+
     for epoch in range(start_epoch, args.maxEpoches):
         if sbm:
             db.epoch(epoch)
@@ -331,25 +342,26 @@ def main(argv=None):
             else:
                 step.load(*ins)
                 loss = step(lrs)
+            # the loss line of this iteration is printed once the NEXT iteration is queued: a
+            # .item() right after the replay would block the host until the step ends, so the
+            # loader's work for the next batch could not overlap the device's step (the recorded
+            # step's loss lives in a buffer the next replay overwrites: keep a device copy)
+            lt = loss.detach().clone()
             if world > 1:
                 # the reference's loss is computed on outputs gathered from the whole global
                 # batch: with equal shards (and the global BCE weight) that is the rank mean
-                lt = loss.detach().clone()
                 dist.all_reduce(lt)
-                lv = float(lt.item()) / world
-            else:
-                lv = float(loss.item())
-            loss_history.append(lv)
-            say("===> Epoch[{}]({}/{}): Loss: {:.10f}  lr: {:.5f}".format(epoch, i_iter, train_len, lv, lr))
-            if logger:
-                logger.write("Epoch[{}]({}/{}):     Loss: {:.10f}      lr: {:.5f}\n".format(
-                    epoch, i_iter, train_len, lv, lr))
-                logger.flush()
+            if pending is not None:
+                report(*pending)
+            pending = (epoch, i_iter, lt, lr)
             del batch, ins
             if args.gc_every_iter:
                 gc.collect()
                 torch.cuda.empty_cache()
             mem(" After GC")
+        if pending is not None:
+            report(*pending)
+            pending = None
         (cache if cache is not None else step).sync_buffers()  # rank 0's BN buffers (DataParallel replica 0)
         if is0:
             path = os.path.join(args.snapshot_dir, "snapshot_%s_%d.pth" % (args.dataset, epoch))
