@@ -104,6 +104,10 @@ def parse():
                          "workload (8 pairs; N = 1 only)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="replay the step as a HIP graph")
+    ap.add_argument("--dp-chain", type=int, default=0,
+                    help="1: run the data-parallel chain (arena, staged encoder backward, bucket "
+                         "pre-scales) at N = 1 without collectives -- configs[2]'s per-rank step "
+                         "timed on one GPU (the line says parallelism dp1-chain)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="data-parallel gradient buckets reduced in fp32 (default) or bf16")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -369,7 +373,8 @@ def main():
     opt = SGD([g0, g1], [0.0, 0.0], momentum=0.9, weight_decay=5e-4)
 
     B, S = args.batch, args.size
-    step = TrainStep(model, opt, B, S, graphed=bool(args.graph), grad_dtype=args.grad_dtype)
+    step = TrainStep(model, opt, B, S, graphed=bool(args.graph), grad_dtype=args.grad_dtype,
+                     dp_chain=bool(args.dp_chain))
     step.load(*[t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)])
     max_iter = 10000
 
@@ -401,8 +406,11 @@ def main():
     t0 = time.perf_counter()
     if prof and not args.graph:
         prof.__enter__()
+    host = []
     for i in range(args.steps):
+        th = time.perf_counter()
         loss = step(lrs(args.warmup + i))
+        host.append(time.perf_counter() - th)
     if prof and not args.graph:
         prof.__exit__()
     torch.cuda.synchronize()
@@ -422,6 +430,11 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
+        # host time inside step() per step (issuing the recorded graphs / the eager kernels): the
+        # mean over the timed steps, and the first one (issued onto an idle device, so no queue
+        # back-pressure is in it)
+        "host_issue_ms_per_step": sum(host) / args.steps * 1e3,
+        "host_issue_ms_first": host[0] * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -430,7 +443,8 @@ def main():
         "config": {"workload": "RGBDSegmentation_RAA train step (fwd+loss+bwd+SGD), %dx%d, "
                                "batch %d pairs/GPU" % (S, S, B),
                    "model": "RGBDSegmentation_RAA(Bottleneck,[3,4,23,3],[3,4,6,3],1)",
-                   "global_batch": B * world, "image_hw": [S, S], "parallelism": "dp%d" % world,
+                   "global_batch": B * world, "image_hw": [S, S],
+                   "parallelism": "dp%d" % world + ("-chain" if args.dp_chain and world == 1 else ""),
                    "grad_reduce": "%s buckets overlapped with the encoder backward" % args.grad_dtype
                    if world > 1 else None,
                    "loss": float(loss.item())},

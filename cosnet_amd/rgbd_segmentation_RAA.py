@@ -184,20 +184,14 @@ class RGBDSegmentation_RAA(nn.Module):
                 cur = torch.cuda.current_stream(rgbs_a.device)
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
-                    da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
-                    dz_a, dz_b = self._depth_head(da, db, dgeo)
-                va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
-                with torch.no_grad():
-                    labels = self.encoder.annotate_nhwc(vb, geo, input_size)   # frame b (:146)
-                z_a, z_b = self._rgb_head(va, vb, geo)
+                    da, db, dgeo, dz_a, dz_b = self.depth_side(depths_a, depths_b)
+                va, vb, geo, labels, z_a, z_b = self.rgb_side(rgbs_a, rgbs_b, input_size)
                 cur.wait_stream(side)
                 for t in (depths_a, depths_b):
                     t.record_stream(side)
                 for t in (da, db, dz_a, dz_b):
                     t.record_stream(cur)
-                if dgeo != geo:
-                    raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
-                x1, x2 = self._decode(z_a, z_b, dz_a, dz_b, geo, input_size)
+                x1, x2 = self.decode_outputs(z_a, z_b, dz_a, dz_b, geo, dgeo, input_size)
                 if stages is not None:
                     stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
                 return x1, x2, labels
@@ -218,6 +212,29 @@ class RGBDSegmentation_RAA(nn.Module):
         if stages is not None:
             stages.update(V_a=va, V_b=vb, D_a=da, D_b=db, geo=geo)
         return x1, x2, labels
+
+    # The two independent halves of the paired forward up to the fusion (:143-191 and :197-247).
+    # forward() runs them on two streams; TrainStep's per-phase recordings call the same two
+    # methods, one graph each, so the cut points cannot drift from forward().
+    def rgb_side(self, rgbs_a, rgbs_b, input_size):
+        """RGB encoder of both frames, labels (frame b, :146) and the RGB head."""
+        va, vb, geo = encode_pair(self.encoder, rgbs_a, rgbs_b)
+        with torch.no_grad():
+            labels = self.encoder.annotate_nhwc(vb, geo, input_size)
+        z_a, z_b = self._rgb_head(va, vb, geo)
+        return va, vb, geo, labels, z_a, z_b
+
+    def depth_side(self, depths_a, depths_b):
+        """Depth encoder of both frames and the depth head."""
+        da, db, dgeo = encode_pair(self.depth_encoder, depths_a, depths_b)
+        dz_a, dz_b = self._depth_head(da, db, dgeo)
+        return da, db, dgeo, dz_a, dz_b
+
+    def decode_outputs(self, z_a, z_b, dz_a, dz_b, geo, dgeo, input_size):
+        """Fusion + decoder of the two halves (:251-266)."""
+        if dgeo != geo:
+            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
+        return self._decode(z_a, z_b, dz_a, dz_b, geo, input_size)
 
     def head_nhwc(self, va, vb, da, db, geo, input_size):
         """Co-attention (RGB and depth), gated fusion and decoder from encoder features

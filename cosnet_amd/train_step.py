@@ -15,16 +15,19 @@ the learning rates in a device tensor refreshed before each replay, and the BCE 
 counts (the only data-dependent scalar of the step) are computed ahead of the graph — under
 data parallelism they are all-reduced there, so the graph itself holds no collective.
 
-Data parallel (world > 1): every gradient lives in one flat fp32 "arena" laid out in the order
-the backward produces it, cut into buckets: [head (co-attention, fusion, decoder)] then the
-depth encoder and the RGB encoder segment by segment ([ASPP + layer4], layer3 halves,
-[layer2 + layer1 + stem]).  The encoder backwards are deferred out of autograd
-(encoder_fn.DeferredEncoderBwd) and write their gradients straight into their bucket, so
-nothing is packed.  The step is recorded as a chain of HIP graphs -- forward + autograd
-backward of the head, then one graph per encoder segment, then SGD -- and each bucket's
-all-reduce (RCCL, async, pre-scaled by 1/world and summed = DataParallel's mean) is issued on
-the host as soon as its graph is queued: bucket k reduces over xGMI while segment k+1
-computes.  Optionally the buckets are reduced in bf16 (grad_dtype="bf16": half the bytes).
+The step is recorded as a program of ONE-STREAM graphs cut at its cross-stream edges (the depth
+side runs on a second stream): a graph with a forked branch blocks the host for its whole replay
+on this ROCm, one-stream graphs joined by events outside the graphs do not (_program).
+
+Data parallel (world > 1): every gradient lives in one flat fp32 "arena", cut into buckets:
+[RGB head + decoder], [depth head], then each encoder segment by segment ([ASPP + layer4],
+layer3 (halves for the RGB encoder), [layer2 + layer1 + stem]).  The encoder backwards are
+deferred out of autograd (encoder_fn.DeferredEncoderBwd) and write their gradients straight
+into their bucket, so nothing is packed.  Each segment is one graph on its encoder's stream, and
+its bucket's all-reduce (RCCL, async, pre-scaled by 1/world and summed = DataParallel's mean) is
+issued on the host as soon as that graph is queued: bucket k reduces over xGMI while the later
+segments compute.  Optionally the buckets are reduced in bf16 (grad_dtype="bf16": half the
+bytes).  dp_chain=True runs the same chain at world 1 without collectives (timing / tracing).
 BN running statistics stay per rank during training (train-mode BN normalises with batch
 statistics, so they never enter the step); sync_buffers() broadcasts rank 0's before evaluation
 or checkpointing.
@@ -43,23 +46,28 @@ class TrainStep:
     """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
 
     def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None,
-                 grad_dtype="fp32", split_graphs=None):
+                 grad_dtype="fp32", split_graphs=None, dp_chain=None):
         self.model, self.opt = model, opt
-        # split_graphs (single process, encoders on two streams): record the step as one-stream
-        # graphs per phase and stream instead of one graph with a forked branch (_split_capture).
-        # ROCm's launch of a multi-stream graph blocks the host for ~the replay's duration; the
-        # one-stream graphs return at once (0.8 ms per step), so the host's own work between
-        # steps (the loader's decode / augmentation in train.py) overlaps the device's step.  The
-        # device time per step is the same either way (profiles/r04_split_graphs_ab.txt).
+        # split_graphs (encoders on two streams): record the step as one-stream graphs per phase
+        # and stream (_program) instead of one graph with a forked branch.  ROCm's launch of a
+        # multi-stream graph blocks the host for ~the replay's duration; the one-stream graphs
+        # return at once (0.8 ms per step), so the host's own work between steps (train.py's
+        # loader; its loss line is read one step late) overlaps the device's step.  The device
+        # time per step is the same either way (profiles/r04_split_graphs_ab.txt).
         if split_graphs is None:
             split_graphs = os.environ.get("CN_SPLIT_GRAPHS", "1") == "1"
         self.split_graphs = bool(split_graphs)
-        self._split = None
         self.grad_dtype = grad_dtype
         self.l1 = float(l1_weight)
         self.graphed = graphed
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        # dp_chain: the data-parallel chain (gradient arena, staged encoder backward, per-bucket
+        # pre-scale) at world 1, without collectives -- configs[2]'s per-rank step, timed and
+        # traced on one GPU (bench.py --dp-chain 1).  CN_DP_CHAIN=1 sets it.
+        if dp_chain is None:
+            dp_chain = os.environ.get("CN_DP_CHAIN", "0") == "1"
+        self.dp_mode = self.world > 1 or bool(dp_chain)
         dev = next(model.parameters()).device
         b = batch
         h, w = (size, size) if isinstance(size, int) else tuple(size)
@@ -87,7 +95,8 @@ class TrainStep:
                     seen.add(id(p))
                     self.params.append(p)
         self.flat = None
-        self.graph = None
+        self.graph = None         # first recorded graph (None: not recorded)
+        self._rec = None          # recorded program: [("graph", role, g) | host actions]
         self._nbt_delta = None
         self.dp = None            # data-parallel state (_dp_setup)
         opt.reserve()  # pinned SGD tables + the device learning-rate tensor
@@ -120,7 +129,7 @@ class TrainStep:
         cur.wait_stream(self.stream)
         return r
 
-    # ---- the recorded body -------------------------------------------------------------------
+    # ---- the one-piece body (eager single-process step, or one graph when not split) ---------
     def _body(self):
         self.opt.zero_grad()
         x1, x2, _ = self.model(self.rgb_a, self.rgb_b, self.dep_a, self.dep_b)
@@ -132,86 +141,164 @@ class TrainStep:
         self.loss = loss.detach()
         self.opt.step()
 
-    # ---- split recording: one-stream graphs per phase and stream -------------------------------
-    def _split_ok(self):
+    # ---- the step as a program of one-stream pieces ------------------------------------------
+    def _side(self):
+        """The depth side's stream (None: the model runs its encoders on one stream)."""
         m = self.model
-        return (self.split_graphs and self.world == 1 and self.stream is not None
-                and getattr(m, "pair_encoder", False) and getattr(m, "no_grad_for_counterpart", False)
-                and m._side_stream(self.rgb_a.device) is not None
-                and self.rgb_a.shape == self.rgb_b.shape)
+        if self.stream is None or not (getattr(m, "pair_encoder", False)
+                                       and getattr(m, "no_grad_for_counterpart", False)
+                                       and self.rgb_a.shape == self.rgb_b.shape):
+            return None
+        return m._side_stream(self.rgb_a.device)
 
-    def _split_capture(self, s1):
-        """The step as six one-stream graphs, the model's forward / backward cut at its four
-        cross-stream edges (rgbd_segmentation_RAA.forward: depth encoder + depth head on the side
-        stream, joined before the decoder; autograd runs their backward there too):
-            s1: A  RGB encoder + RGB head       s2: A' depth encoder + depth head
-            s1: B  decoder + loss + their backward (gradients of the three head outputs)
-            s1: C  RGB head + encoder backward  s2: C' depth head + encoder backward
-            s1: D  SGD
-        Each stream's graphs draw on a pool of their own: a graph of one stream never reuses
-        memory a concurrently running graph of the other stream still holds.  The kernels and
-        their order per stream are those of the one-graph recording (bitwise-equal results,
-        tests/test_gpu_train_step.py)."""
-        from .encoder_fn import encode_pair
+    def _split_ok(self):
+        return self.split_graphs and self.world == 1 and not self.dp_mode and self._side() is not None
+
+    def _program(self):
+        """The step cut at its cross-stream edges into one-stream pieces, in issue order:
+            ("run", role, fn)         -- device work on stream `role` ("s1": the step's stream,
+                                         "s2": the depth side's); ONE graph when recorded
+            ("join", dst, src)        -- dst waits for src's queued work (outside the graphs)
+            ("reduce", k, role)       -- bucket k's async all-reduce, issued from `role`
+            ("finish",)               -- the step's stream waits for every issued all-reduce
+        Forward: depth side (s2) | RGB side (s1) -- the model's rgb_side / depth_side, the same
+        cut points as its forward(); then decoder + loss + their gradients (s1); the backward of
+        each side on its own stream; SGD (s1).  Data parallel: each side's head backward ends with
+        its head bucket and only stashes the encoder's feature gradient (DeferredEncoderBwd); the
+        encoder backwards then run segment by segment (one piece each, RGB on s1 beside depth on
+        s2), every piece ending with its bucket's pre-scale, and the host issues that bucket's
+        all-reduce right after queuing it, so it runs over xGMI beside the later segments."""
         m = self.model
-        s2 = m._side_stream(self.rgb_a.device)
-        p1, p2 = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+        dp = self.dp_mode
+        env = {}
         isz = tuple(self.rgb_a.shape[2:])
-        self.opt.zero_grad()
-        m._set_dtype()
-        s2.wait_stream(s1)
-        gA, hA, gB, gC, hC, gD = (torch.cuda.CUDAGraph() for _ in range(6))
-        with torch.cuda.graph(gA, stream=s1, pool=p1):
-            va, vb, geo = encode_pair(m.encoder, self.rgb_a, self.rgb_b)
-            with torch.no_grad():
-                m.encoder.annotate_nhwc(vb, geo, isz)                      # labels (:146)
-            z_a, z_b = m._rgb_head(va, vb, geo)
-        with torch.cuda.graph(hA, stream=s2, pool=p2):
-            da, db, dgeo = encode_pair(m.depth_encoder, self.dep_a, self.dep_b)
-            dz_a, dz_b = m._depth_head(da, db, dgeo)
-        if dgeo != geo:
-            raise RuntimeError("RGB and depth feature maps differ: %s vs %s" % (geo, dgeo))
-        outs = [t for t in (z_a, z_b, dz_a) if t.requires_grad]
-        dec = [p for mod in (m.segmentation_classifier_A, m.segmentation_classifier_B)
-               for p in mod.parameters() if p.requires_grad]
-        with torch.cuda.graph(gB, stream=s1, pool=p1):
-            x1, x2 = m._decode(z_a, z_b, dz_a, dz_b, geo, isz)
+
+        def dep_fwd():
+            env["d"] = m.depth_side(self.dep_a, self.dep_b)
+
+        def rgb_fwd():
+            env["r"] = m.rgb_side(self.rgb_a, self.rgb_b, isz)
+
+        def decode():
+            va, vb, geo, labels, z_a, z_b = env["r"]
+            da, db, dgeo, dz_a, dz_b = env["d"]
+            x1, x2 = m.decode_outputs(z_a, z_b, dz_a, dz_b, geo, dgeo, isz)
             loss = fn.BceL1PairDevFn.apply(x1, x2, self.gt_a, self.gt_b, self.cnt, self.total, self.l1)
+            self._mem(" After forward")
+            outs = [t for t in (z_a, z_b, dz_a) if t.requires_grad]
+            dec = [p for mod in (m.segmentation_classifier_A, m.segmentation_classifier_B)
+                   for p in mod.parameters() if p.requires_grad]
             grads = torch.autograd.grad(loss, outs + dec, self._one)
             for p, g in zip(dec, grads[len(outs):]):
                 p.grad = g
-        gout = dict(zip([id(t) for t in outs], grads[:len(outs)]))
-        rgb = [(t, gout[id(t)]) for t in (z_a, z_b) if id(t) in gout]
-        with torch.cuda.graph(gC, stream=s1, pool=p1):
-            torch.autograd.backward([t for t, _ in rgb], [g for _, g in rgb])
-        with torch.cuda.graph(hC, stream=s2, pool=p2):
-            if id(dz_a) in gout:
-                torch.autograd.backward([dz_a], [gout[id(dz_a)]])
-        with torch.cuda.graph(gD, stream=s1, pool=p1):
-            self.opt.step()
-        self.loss = loss.detach()
-        # the graphs read these across their boundaries: keep them (and their memory) alive
-        self._split = {"s2": s2, "g": (gA, hA, gB, gC, hC, gD),
-                       "keep": (va, vb, z_a, z_b, da, db, dz_a, dz_b, x1, x2, grads)}
-        self.graph = gA
+            env["gout"] = dict(zip([id(t) for t in outs], grads[:len(outs)]))
+            env["loss"] = loss.detach()
+            env["x"] = (x1, x2)
 
-    def _split_replay(self):
-        sp = self._split
-        s2 = sp["s2"]
-        gA, hA, gB, gC, hC, gD = sp["g"]
-        cur = torch.cuda.current_stream()
-        s2.wait_stream(cur)              # inputs, counts and learning rates of this step
-        with torch.cuda.stream(s2):
-            hA.replay()
-        gA.replay()
-        cur.wait_stream(s2)
-        gB.replay()
-        s2.wait_stream(cur)
-        with torch.cuda.stream(s2):
-            hC.replay()
-        gC.replay()
-        cur.wait_stream(s2)
-        gD.replay()
+        def rgb_bwd():
+            z_a, z_b = env["r"][4], env["r"][5]
+            rgb = [(t, env["gout"][id(t)]) for t in (z_a, z_b) if id(t) in env["gout"]]
+            torch.autograd.backward([t for t, _ in rgb], [g for _, g in rgb])
+            if dp:
+                self._dp_head_bucket(0)
+
+        def dep_bwd():
+            dz_a = env["d"][3]
+            if id(dz_a) in env["gout"]:
+                torch.autograd.backward([dz_a], [env["gout"][id(dz_a)]])
+            if dp:
+                self._dp_head_bucket(1)
+
+        def sgd():
+            if dp:
+                self._dp_sgd()
+            else:
+                self.opt.step()
+            self._mem(" After backward")
+
+        prog = [("join", "s2", "s1"), ("run", "s2", dep_fwd), ("run", "s1", rgb_fwd),
+                ("join", "s1", "s2"), ("run", "s1", decode), ("join", "s2", "s1"),
+                ("run", "s2", dep_bwd)]
+        if dp:
+            prog.append(("reduce", 1, "s2"))
+        prog.append(("run", "s1", rgb_bwd))
+        if dp:
+            prog.append(("reduce", 0, "s1"))
+            for d, k, bk, role in self.dp["pieces"]:
+                prog += [("run", role, self._dp_piece(d, k, bk)), ("reduce", bk, role)]
+        prog.append(("join", "s1", "s2"))
+        if dp:
+            prog.append(("finish",))
+        prog.append(("run", "s1", sgd))
+        return prog, env
+
+    def _streams(self):
+        s1 = torch.cuda.current_stream()
+        s2 = self._side()
+        return {"s1": s1, "s2": s2 if s2 is not None else s1}
+
+    def _host_op(self, op, S):
+        if op[0] == "join":
+            if S[op[1]] is not S[op[2]]:
+                S[op[1]].wait_stream(S[op[2]])
+        elif op[0] == "reduce":
+            with torch.cuda.stream(S[op[2]]):
+                self._dp_launch_reduce(op[1])
+        elif op[0] == "finish":
+            for w in self.dp["works"]:
+                w.wait()
+            self.dp["works"] = []
+
+    def _run_program(self):
+        """One eager step through the program (data parallel / forced chain; the warm-up and
+        run_batch path of that mode), on the caller's current stream as s1."""
+        prog, env = self._program()
+        S = self._streams()
+        self.opt.zero_grad()
+        self.model._set_dtype()
+        for op in prog:
+            if op[0] == "run":
+                with torch.cuda.stream(S[op[1]]):
+                    op[2]()
+            else:
+                self._host_op(op, S)
+        # tensors handed across the streams stay alive in `env` until every piece has run (the
+        # final join orders both streams before SGD); nothing is freed while the other stream uses it
+        self.loss = env["loss"]
+        self._env_eager = env
+
+    def _record_program(self):
+        """Record each piece as one graph on its stream; a memory pool per stream, so a graph never
+        reuses memory that a concurrently running graph of the other stream still holds.  The
+        pieces' tensors stay referenced (env) for the life of the recording."""
+        prog, env = self._program()
+        S = {"s1": self.stream, "s2": self._side() or self.stream}
+        pools = {"s1": torch.cuda.graph_pool_handle()}
+        pools["s2"] = pools["s1"] if S["s2"] is S["s1"] else torch.cuda.graph_pool_handle()
+        self.opt.zero_grad()
+        self.model._set_dtype()
+        rec = []
+        for op in prog:
+            if op[0] == "run":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=S[op[1]], pool=pools[op[1]]):
+                    op[2]()
+                rec.append(("graph", op[1], g))
+            else:
+                rec.append(op)
+        self._rec = rec
+        self._rec_env = env
+        self.loss = env["loss"]
+        self.graph = next(o[2] for o in rec if o[0] == "graph")
+
+    def _replay_program(self):
+        S = self._streams()
+        for op in self._rec:
+            if op[0] == "graph":
+                with torch.cuda.stream(S[op[1]]):
+                    op[2].replay()
+            else:
+                self._host_op(op, S)
 
     # ---- data parallel: arena, buckets, deferred encoder backward ----------------------------
     def _bind(self):
@@ -222,23 +309,30 @@ class TrainStep:
                 e._cn_defer = d
 
     def _dp_setup(self):
+        """Gradient arena and buckets: [RGB head + decoder], [depth head], then one bucket per
+        encoder-backward segment of each encoder (RGB: [ASPP + layer4], layer3 halves, [layer2 +
+        layer1 + stem]; depth: [ASPP + layer4], layer3, [layer2 + layer1 + stem]).  `pieces` =
+        (holder, segment, bucket, stream role) in issue order: depth segment j, then RGB segment
+        j -- each side's segments follow each other on its own stream."""
         from .encoder_fn import DeferredEncoderBwd
         m = self.model
         train = [p for p in self.params]
+        tid = {id(p) for p in train}
         encs = [m.encoder, m.depth_encoder]
         defers = [DeferredEncoderBwd(e, None) for e in encs]
         enc_ids = {id(p) for e in encs for p in e.parameters()}
-        head = [p for p in train if id(p) not in enc_ids]
-        buckets = [head]
-        # stage j = RGB segment j (on the step's stream) beside depth segment j (on the model's
-        # second stream, as in the forward); one bucket per stage, all-reduced while the next
-        # stage computes
-        segs = []
+        dep_mods = [m.depth_similarity_weights, m.depth_gate, m.depth_reduce_channels, m.depth_bn,
+                    m.depth_weights]
+        dep_ids = {id(p) for mod in dep_mods for p in mod.parameters()}
+        head_rgb = [p for p in train if id(p) not in enc_ids and id(p) not in dep_ids]
+        head_dep = [p for p in train if id(p) in dep_ids]
+        buckets = [head_rgb, head_dep]
+        pieces = []
         for j in range(max(len(d.plan) for d in defers)):
-            st = [(d, j) for d in defers if j < len(d.plan)]
-            ps = [p for d, k in st for p in d.segment_params(k) if any(p is q for q in train)]
-            buckets.append(ps)
-            segs.append(st)
+            for d, role in ((defers[1], "s2"), (defers[0], "s1")):
+                if j < len(d.plan):
+                    pieces.append((d, j, len(buckets), role))
+                    buckets.append([p for p in d.segment_params(j) if id(p) in tid])
         got = [p for b in buckets for p in b]
         assert len({id(p) for p in got}) == len(got), "a parameter in two buckets"
         missing = [p for p in train if id(p) not in {id(q) for q in got}]
@@ -264,25 +358,27 @@ class TrainStep:
         half = None
         if self.grad_dtype == "bf16":
             half = torch.zeros((n,), dtype=torch.bfloat16, device=dev)
-        self.dp = {"buckets": buckets, "ranges": ranges, "segs": segs, "flat": flat, "arena": arena,
-                   "views": views, "head": head, "half": half, "works": [], "graphs": None,
-                   "head_live": None, "defers": defers}
+        self.dp = {"buckets": buckets, "ranges": ranges, "pieces": pieces, "flat": flat,
+                   "arena": arena, "views": views, "half": half, "works": [],
+                   "head_live": [None, None], "defers": defers}
         self.flat = flat
 
-    def _dp_forward_backward(self):
-        """Graph A's body: forward, loss, autograd backward (encoders deferred), head bucket."""
+    def _dp_head_bucket(self, k):
+        """Head bucket k (0: RGB head + decoder, 1: depth head): copy the autograd gradients into
+        the arena and ready the bucket for its all-reduce."""
         dp = self.dp
-        self.opt.zero_grad()
-        x1, x2, _ = self.model(self.rgb_a, self.rgb_b, self.dep_a, self.dep_b)
-        loss = fn.BceL1PairDevFn.apply(x1, x2, self.gt_a, self.gt_b, self.cnt, self.total, self.l1)
-        self._mem(" After forward")
-        torch.autograd.backward(loss, self._one)
-        self.loss = loss.detach()
-        if dp["head_live"] is None:   # which head parameters receive a gradient (static)
-            dp["head_live"] = [p for p in dp["head"] if p.grad is not None]
-        live = dp["head_live"]
-        torch._foreach_copy_([dp["views"][p] for p in live], [p.grad for p in live])
-        self._dp_prepare_bucket(0)
+        if dp["head_live"][k] is None:   # which head parameters receive a gradient (static)
+            dp["head_live"][k] = [p for p in dp["buckets"][k] if p.grad is not None]
+        live = dp["head_live"][k]
+        if live:
+            torch._foreach_copy_([dp["views"][p] for p in live], [p.grad for p in live])
+        self._dp_prepare_bucket(k)
+
+    def _dp_piece(self, d, k, bk):
+        def piece():
+            d.run(k)
+            self._dp_prepare_bucket(bk)
+        return piece
 
     def _dp_prepare_bucket(self, k):
         """Device work that readies bucket k for its all-reduce: the 1/world pre-scale (sum of
@@ -295,69 +391,27 @@ class TrainStep:
         if dp["half"] is not None:
             ops.cast_copy(dp["flat"][a:b].view(-1, 1), dp["half"][a:b].view(-1, 1))
 
-    def _dp_stage(self, i):
-        """Encoder-backward stage i: the RGB segment here, the depth segment on the side stream."""
-        st = self.dp["segs"][i]
-        # the stream follows the ENCODER, not the position in the stage: the depth segments'
-        # saved activations were allocated on the side stream by the forward
-        depth = getattr(self.model.depth_encoder, "_cn_defer", None)
-        on_side = [(d, k) for d, k in st if d is depth]
-        here = [(d, k) for d, k in st if d is not depth]
-        side = self.model._side_stream(self.flat.device) if on_side else None
-        if side is None:
-            for d, k in st:
-                d.run(k)
-            return
-        cur = torch.cuda.current_stream()
-        side.wait_stream(cur)
-        for d, k in here:
-            d.run(k)
-        with torch.cuda.stream(side):
-            for d, k in on_side:
-                d.run(k)
-        cur.wait_stream(side)
-
-    def _dp_segment(self, i):
-        self._dp_stage(i)
-        self._dp_prepare_bucket(i + 1)
-
     def _dp_launch_reduce(self, k):
         """Issue bucket k's all-reduce (async): RCCL waits for the work queued so far on the
-        current stream and runs beside the segments queued after it."""
+        current stream and runs beside the pieces queued after it.  World 1 (forced chain): none."""
         dp = self.dp
         a, b = dp["ranges"][k]
-        if b == a:
+        if b == a or self.world == 1:
             return
         buf = dp["half"][a:b] if dp["half"] is not None else dp["flat"][a:b]
         dp["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
 
-    def _dp_finish(self):
-        """Wait for every bucket, (cast back,) point the parameters' .grad at the arena, SGD."""
-        dp = self.dp
-        for w in dp["works"]:
-            w.wait()
-        dp["works"] = []
-        self._dp_sgd()
-
     def _dp_sgd(self):
+        """(Cast the reduced bf16 buckets back,) point the parameters' .grad at the arena, SGD."""
         dp = self.dp
         if dp["half"] is not None:
             ops.cast_copy(dp["half"].view(-1, 1), dp["flat"].view(-1, 1))
-        live = set(id(p) for p in dp["head_live"])
+        live = set(id(p) for k in (0, 1) for p in (dp["head_live"][k] or []))
         for b_i, b in enumerate(dp["buckets"]):
             for p in b:
-                if b_i > 0 or id(p) in live:
+                if b_i > 1 or id(p) in live:
                     p.grad = dp["views"][p]
         self.opt.step()
-        self._mem(" After backward")
-
-    def _dp_eager_once(self):
-        self._dp_forward_backward()
-        self._dp_launch_reduce(0)
-        for i in range(len(self.dp["segs"])):
-            self._dp_segment(i)
-            self._dp_launch_reduce(i + 1)
-        self._dp_finish()
 
     # ---- capture / replay ---------------------------------------------------------------------
     def _bn_counts(self):
@@ -366,7 +420,7 @@ class TrainStep:
 
     def capture(self, warmup=2):
         """Run `warmup` eager iterations (they are real steps) on a side stream, then record."""
-        if self.world > 1 and self.dp is None:
+        if self.dp_mode and self.dp is None:
             self._dp_setup()
         self._bind()
         if not self.graphed:
@@ -389,10 +443,8 @@ class TrainStep:
         before = self._bn_counts()
         self._capturing = True
         try:
-            if self.world > 1:
-                self._dp_capture(s)
-            elif self._split_ok():
-                self._split_capture(s)
+            if self.dp_mode or self._split_ok():
+                self._record_program()
             else:
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph, stream=s):
@@ -408,49 +460,12 @@ class TrainStep:
             m._cn_nbt = k
         torch.cuda.synchronize()
 
-    def _dp_capture(self, s):
-        """Record the data-parallel step as a chain of graphs sharing one memory pool: A (forward
-        + autograd backward + head bucket), one per encoder segment, and SGD.  The tensors the
-        later graphs read (saved activations, the stashed feature gradients) stay referenced
-        by the deferred-backward holders, so no capture reuses their memory."""
-        dp = self.dp
-        pool = torch.cuda.graph_pool_handle()
-        keep = []
-        ga = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(ga, stream=s, pool=pool):
-            self._dp_forward_backward()
-        segs = []
-        for i in range(len(dp["segs"])):
-            keep.append([(d.rec, d.dfa) for d, _ in dp["segs"][i]])
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, pool=pool):
-                self._dp_segment(i)
-            segs.append(g)
-        gs = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gs, stream=s, pool=pool):
-            self._dp_sgd()
-        dp["graphs"] = (ga, segs, gs, keep)
-        self.graph = ga
-
-    def _dp_replay(self):
-        dp = self.dp
-        ga, segs, gs, _ = dp["graphs"]
-        ga.replay()
-        self._dp_launch_reduce(0)
-        for i, g in enumerate(segs):
-            g.replay()
-            self._dp_launch_reduce(i + 1)
-        for w in dp["works"]:
-            w.wait()
-        dp["works"] = []
-        gs.replay()
-
     def run_batch(self, rgb_a, rgb_b, dep_a, dep_b, gt_a, gt_b, lrs):
         """One EAGER iteration on inputs of any size (the reference's augmented batches change
         H, W every batch, so they cannot replay one recorded graph)."""
         if self.graphed and self.graph is not None:
             raise RuntimeError("run_batch is the eager path; build the TrainStep with graphed=False")
-        if self.world > 1 and self.dp is None:
+        if self.dp_mode and self.dp is None:
             self._dp_setup()
         b, _, h, w = rgb_a.shape
         self.rgb_a, self.rgb_b, self.dep_a, self.dep_b, self.gt_a, self.gt_b = (
@@ -468,15 +483,15 @@ class TrainStep:
         return self.loss
 
     def _eager_once(self):
-        if self.world > 1 and self.dp is None:
+        if self.dp_mode and self.dp is None:
             self._dp_setup()
         self._bind()
 
         def once():
             self._counts()
             self.opt.refresh_lrs()
-            if self.world > 1:
-                self._dp_eager_once()
+            if self.dp_mode:
+                self._run_program()
             else:
                 self._body()
         self._on_stream(once)
@@ -489,10 +504,8 @@ class TrainStep:
             return self.loss
         self.opt.refresh_lrs()
         self._counts()
-        if self.world > 1:
-            self._dp_replay()
-        elif self._split is not None:
-            self._split_replay()
+        if self._rec is not None:
+            self._replay_program()
         else:
             self.graph.replay()
         self.loss = self._graph_loss

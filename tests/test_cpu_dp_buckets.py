@@ -1,7 +1,8 @@
 """The data-parallel gradient layout and bucket reduction of TrainStep (train_step.py) on CPU,
 world_size 2 over gloo: the arena/bucket plan covers every trainable parameter exactly once,
-stage j's bucket holds exactly RGB segment j + depth segment j (the order the staged encoder
-backward produces them), slots are 64-byte aligned, and the per-bucket async all-reduce sums
+the two head buckets split the RGB head + decoder from the depth head, every encoder segment has
+a bucket of its own holding exactly that segment's parameters in production order, issued from
+its encoder's stream, slots are 64-byte aligned, and the per-bucket async all-reduce sums
 the ranks' 1/world-scaled buckets into DataParallel's mean.  (The pre-scale and the SGD are
 HIP kernels; their GPU coverage is tests/test_gpu_dataparallel.py.)"""
 import os
@@ -48,13 +49,17 @@ def _worker(rank, world, port, q):
         ok_align = all(a % 16 == 0 for a, _ in dp["ranges"])
         ok_contig = all(dp["ranges"][i][1] == dp["ranges"][i + 1][0] for i in range(len(dp["ranges"]) - 1))
         ok_alias = all(dp["views"][p].data_ptr() == dp["arena"][p].data_ptr() for p in got)
-        ok_stage = True
-        for j, st in enumerate(dp["segs"]):
-            encs = [type(d.enc).__name__ for d, _ in st]
-            want = [p for d, k in st for p in d.segment_params(k)
-                    if any(p is q for q in ts.params)]
-            ok_stage &= [id(p) for p in dp["buckets"][j + 1]] == [id(p) for p in want]
-            ok_stage &= encs[0] == "Encoder" and (len(st) == 1 or "Depth" in encs[1])
+        ok_stage = len(dp["pieces"]) == 4 + 3
+        # bucket 0 = RGB head + decoder, bucket 1 = depth head, then one bucket per encoder
+        # segment: depth segment j (depth stream) before RGB segment j (the step's stream)
+        dep_head = {id(p) for mod in (m.depth_similarity_weights, m.depth_gate, m.depth_reduce_channels,
+                                      m.depth_bn, m.depth_weights) for p in mod.parameters()}
+        ok_stage &= {id(p) for p in dp["buckets"][1]} == dep_head
+        ok_stage &= not any(id(p) in dep_head for p in dp["buckets"][0])
+        for i, (d, k, bk, role) in enumerate(dp["pieces"]):
+            want = [p for p in d.segment_params(k) if any(p is q for q in ts.params)]
+            ok_stage &= bk == i + 2 and [id(p) for p in dp["buckets"][bk]] == [id(p) for p in want]
+            ok_stage &= role == ("s2" if "Depth" in type(d.enc).__name__ else "s1")
         # every rank writes (rank + 1) / world into its buckets (the in-graph 1/world pre-scale),
         # the per-bucket async all-reduce must leave the mean (1 + 2) / 2 everywhere
         dp["flat"].fill_((rank + 1) / world)
@@ -64,7 +69,7 @@ def _worker(rank, world, port, q):
             w.wait()
         a, b = dp["ranges"][0][0], dp["ranges"][-1][1]
         red = dp["flat"][a:b]
-        q.put((rank, ok_cover, ok_align, ok_contig, ok_alias, ok_stage, len(dp["segs"]),
+        q.put((rank, ok_cover, ok_align, ok_contig, ok_alias, ok_stage, len(dp["pieces"]),
                float(red.min()), float(red.max())))
     finally:
         dist.destroy_process_group()
@@ -84,5 +89,5 @@ def test_bucket_plan_and_reduction_two_ranks():
         assert p.exitcode == 0
     for rank, cover, align, contig, alias, stage, nseg, lo, hi in res:
         assert cover and align and contig and alias and stage, (rank, cover, align, contig, alias, stage)
-        assert nseg == 4          # RGB: ASPP+layer4, layer3 x2, layer2+1+stem; depth: 3 of them
+        assert nseg == 7          # RGB: ASPP+layer4, layer3 x2, layer2+1+stem; depth: 3 of them
         assert lo == hi == 1.5, (lo, hi)

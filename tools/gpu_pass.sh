@@ -15,6 +15,7 @@
 #   pmc              the PMC traffic passes of tools/pmc_run.sh
 #   smoke            __graft_entry__.smoke()
 #   py:SCRIPT[,ARGS] python SCRIPT ARGS (a tools/ probe or A/B script)
+#   envbench:VAR=VALUE[,ARGS]  bench.py ARGS with one environment variable set (A/B lines)
 set -o pipefail
 NAME=$1; shift
 O=gpurun_out/$NAME
@@ -22,9 +23,11 @@ mkdir -p $O
 export TMPDIR=/tmp
 PY="python -u"
 note() { echo "$*" >> $O/rc.txt; }
+i=0
 for step in "$@"; do
+  i=$((i + 1))
   kind=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
-  tag=$(echo "$step" | tr -c 'A-Za-z0-9_.\n-' '_' | cut -c1-60)
+  tag=$(printf '%02d_' $i)$(echo "$step" | tr -c 'A-Za-z0-9_.\n-' '_' | cut -c1-60)
   case $kind in
     tests)
       if [ -n "$arg" ]; then sel=(-k "$arg"); else sel=(); fi
@@ -48,6 +51,11 @@ for step in "$@"; do
       rc=$?; note "$step rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     py)
       timeout -k 10 600 $PY ${arg//,/ } > $O/$tag.log 2>&1
+      rc=$?; note "$step rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    envbench)
+      # envbench:VAR=VALUE,bench-args...  (one environment variable for an A/B bench line)
+      ev=${arg%%,*}; rest=${arg#*,}
+      env "$ev" timeout -k 10 700 $PY bench.py ${rest//,/ } > $O/$tag.json 2> $O/$tag.err
       rc=$?; note "$step rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     *) note "unknown step $step"; exit 2 ;;
   esac

@@ -39,7 +39,11 @@ def main(path):
             else:
                 ce = max(ce, e)
         un += ce - cs
-        print(f"  device busy (union) {un / 1e6:.2f} ms, idle {(t1 - t0 - un) / 1e6:.2f} ms")
+        # idle before the step's first kernel, after the previous step's SGD (host issue gaps of
+        # the program's graphs and host-issued kernels show up here)
+        lead = t0 - int(rows[a]["End_Timestamp"])
+        print(f"  device busy (union) {un / 1e6:.2f} ms, idle {(t1 - t0 - un) / 1e6:.2f} ms, "
+              f"idle before the step {lead / 1e6:.3f} ms, period {(t1 - int(rows[a]['End_Timestamp'])) / 1e6:.2f} ms")
 
 
 if __name__ == "__main__":
