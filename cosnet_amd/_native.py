@@ -113,6 +113,9 @@ _SIGS = {
     "cn_cast2d": (_I, [_I, _I, _P, _L, _I, _I, _P, _L, _I, _P]),
     "cn_build_source_hash": (ctypes.c_char_p, []),
     "cn_build_experimental": (_I, []),
+    "cn_conv_wgrad_fp8_workspace_floats": (_S, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "cn_conv_wgrad_fp8": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _L, _I, _I, _I, _I, _I, _I, _I, _I,
+                               _P, _P, _P, _P, _S, _P]),
 }
 
 _lib = None

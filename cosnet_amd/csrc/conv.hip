@@ -28,7 +28,9 @@ static ConvGeom make_geom(int N, int H, int W, int C, int OH, int OW, int KH, in
   return g;
 }
 
-static int vec_of(int dtype) { return dtype == DT_BF16 ? 8 : 4; }
+static int vec_of(int dtype) {
+  return dtype == DT_BF16 ? 8 : (dtype == DT_FP8 || dtype == DT_FP8_E5M2) ? 16 : 4;
+}
 
 // zero-fill with 16-byte vector stores (a kernel, not a memset node, inside captured graphs)
 __global__ void zero16_k(u32x4* p, long long n16) {
@@ -357,7 +359,21 @@ static void wgrad_plan(int dtype, int N, int OH, int OW, int Cout, int KH, int K
   int BK = 8 * vec_of(dtype);
   long long tiles;
   int target = g_wgrad_target;
-  if (dtype == DT_BF16) {
+  if (dtype == DT_FP8_E5M2) {
+    // fp8 operands: 128x128 / 8 waves (the k-major fp8 reader's tile), the bf16 block target
+    *cfg = 11;
+    tiles = cn_gemm_cfg_blocks(11, M, NN) * G;
+    if (target == 512) {
+      if (tiles >= 256) target = 1024;
+      else {
+        long long s = 512 / tiles;
+        long long maxs = K / (8 * BK);
+        if (s > maxs) s = maxs;
+        if (s < 1) s = 1;
+        target = (int)(s * tiles);
+      }
+    }
+  } else if (dtype == DT_BF16) {
     // 128x128 / 8 waves (tools/wgrad_sweep.sh); the narrow layer-1 products get tiles that
     // do not waste half their MFMAs: 128x64 for N <= 64, 64x128 for Cout <= 64
     *cfg = NN <= 64 ? 12 : (M <= 64 ? 17 : 11);
@@ -553,6 +569,82 @@ extern "C" int cn_conv_wgrad_grouped_ws(int dtype, int G, const void* const* xs,
   a.slab = slab;
   int rc = cn_gemm_dispatch(a, dtype, 1, L_MC_DENSE, lb, G, st);
   if (rc) return rc;
+  RedOut o;
+  for (int g = 0; g < G; ++g) o.out[g] = dws[g];
+  const long long n4 = slab / 4;
+  long long bx = (n4 + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(splitk_reduce_grouped_k, dim3((unsigned)bx, G), dim3(256), 0, st, (const float*)ws,
+                     ns, slab, n4, o);
+  CN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- fp8 weight gradients (BASELINE configs[4]) ------------------------------------------------
+// dW[g] fp32 [Cout][KH][KW][Cin] = sum over output pixels of dY8[g] (e5m2) x im2col(X8[g]) (e4m3) *
+// dy_scale[g] * x_scale[g]: the weight gradients of G convs of one shape in one launch (G = 1: a
+// single conv), both operands k-major (pixel rows) -- the e5m2 output gradient the fp8 dgrad
+// already quantised and the e4m3 input copy the fp8 forward conv read -- on the block-scaled
+// 16x16x128 MFMA (A e5m2, B e4m3, unit block scales) with transposed byte reads of the LDS tiles
+// (gemm.hip read_frag_f8_mc).  Split over K into fp32 slabs when the group does not fill the chip
+// (wgrad_plan), summed in split order by one reduce launch (deterministic).
+extern "C" size_t cn_conv_wgrad_fp8_workspace_floats(int G, int N, int OH, int OW, int Cout, int KH,
+                                                     int KW, int Cin) {
+  if (G < 1) return 0;
+  int ns, ch, cfg;
+  wgrad_plan(DT_FP8_E5M2, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg, G);
+  return ns > 1 ? (size_t)G * ns * Cout * KH * KW * Cin : 0;
+}
+
+extern "C" int cn_conv_wgrad_fp8(int G, const void* const* xs8, long long ldx, int N, int H, int W,
+                                 int Cin, const void* const* dys8, long long lddy, int OH, int OW,
+                                 int Cout, int KH, int KW, int stride, int pad, int dil,
+                                 float* const* dws, const float* const* x_states,
+                                 const float* const* dy_states, float* ws, size_t ws_floats,
+                                 hipStream_t st) {
+  if (G < 1 || G > GEMM_MAXG) return CN_ERR_SHAPE;
+  if (Cin % 16 || Cout % 16 || ldx % 16 || lddy % 16) return CN_ERR_ALIGN;
+  for (int g = 0; g < G; ++g)
+    if (((uintptr_t)xs8[g] & 15) || ((uintptr_t)dys8[g] & 15) || ((uintptr_t)dws[g] & 15) ||
+        !x_states[g] || !dy_states[g])
+      return CN_ERR_ALIGN;
+  int ns, ch, cfg;
+  wgrad_plan(DT_FP8_E5M2, N, OH, OW, Cout, KH, KW, Cin, &ns, &ch, &cfg, G);
+  const long long slab = (long long)Cout * KH * KW * Cin;
+  const bool split = ns > 1;
+  if (split && (!ws || ws_floats < (size_t)G * ns * slab || ((uintptr_t)ws & 15) || slab % 4))
+    return CN_ERR_SHAPE;
+  GemmArgs a = gemm_defaults();
+  a.M = Cout; a.N = KH * KW * Cin; a.K = N * OH * OW;
+  a.ka_lim = a.kb_lim = a.K;
+  a.lda = lddy;
+  a.ldb = ldx;
+  a.ldc = a.N;
+  int lb = L_MC_DENSE;
+  if (!(KH == 1 && KW == 1 && stride == 1 && pad == 0)) {
+    lb = L_MC_CONV;
+    a.gb = make_geom(N, H, W, Cin, OH, OW, KH, KW, stride, -pad, -pad, dil, dil);
+  }
+  a.ngroup = G;
+  for (int g = 0; g < G; ++g) {
+    a.grp.A[g] = dys8[g];
+    a.grp.B[g] = xs8[g];
+    a.grp.C[g] = split ? (void*)(ws + (long long)g * ns * slab) : (void*)dws[g];
+    a.grp.SA[g] = dy_states[g];   // state[0] = dequantisation scale
+    a.grp.SB[g] = x_states[g];
+  }
+  a.A = dys8[0]; a.B = xs8[0]; a.C = a.grp.C[0];
+  if (split) {
+    a.cfg = 11;
+    a.nsplit = ns;
+    a.k_chunk = ch;
+    a.c_mode = 3;
+    a.slab = slab;
+  } else {
+    a.cfg = 13;   // every block runs the whole K: the 3-deep ring (as the bf16 groups)
+  }
+  int rc = cn_gemm_dispatch(a, DT_FP8_E5M2, 1, L_MC_DENSE, lb, G, st);
+  if (rc || !split) return rc;
   RedOut o;
   for (int g = 0; g < G; ++g) o.out[g] = dws[g];
   const long long n4 = slab / 4;

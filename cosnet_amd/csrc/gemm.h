@@ -29,6 +29,9 @@ struct GemmGroup {
   const void* A[GEMM_MAXG];
   const void* B[GEMM_MAXG];
   void* C[GEMM_MAXG];
+  // fp8 operands: per-problem dequantisation scales (null: the launch-wide scale_a / scale_b)
+  const float* SA[GEMM_MAXG];
+  const float* SB[GEMM_MAXG];
 };
 
 struct GemmArgs {

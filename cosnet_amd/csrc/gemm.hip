@@ -35,6 +35,13 @@ __device__ __forceinline__ int mc_swz(int k, int granules_per_row) {
   return (granules_per_row >= 32 ? h : (h & 3)) << 2;
 }
 
+// fp8 MC tiles ([k][128 columns] bytes, eight 16-byte column chunks per k-row): chunk c of k-row k
+// sits in slot c ^ mc_swz8(k).  A ds_read_b64_tr_b8 of one 16-lane group reads eight consecutive
+// k-rows of one chunk (read_frag_f8_mc): k & 7 spreads them over eight slots, and (k >> 5) & 1
+// moves the group reading k + 32 to the other eight 16-byte bank groups of the 256-byte window,
+// so the two groups of a half-wave cover all 64 banks once.
+__device__ __forceinline__ int mc_swz8(int k) { return (k & 7) ^ ((k >> 5) & 1); }
+
 // 16 zero bytes in global memory: out-of-bounds lanes of an LDS-DMA fill read from here.
 __device__ __attribute__((aligned(16))) unsigned g_zero16[4];
 
@@ -85,6 +92,7 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
   static constexpr int KROW_STEP = NT / CPR;      // MC: k-rows between a thread's chunks
   static constexpr int RB = ROWS * (int)sizeof(T);  // MC: bytes per k-row of the LDS image
   static constexpr unsigned SZ = sizeof(T);
+  static_assert(!(MC && sizeof(T) == 1) || CPR == 8, "fp8 MC tiles are 128 columns wide (mc_swz8)");
 
   long long ld;
   int klim;             // k bound (zero beyond)
@@ -142,7 +150,8 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int krl = tid / CPR + KROW_STEP * i;  // k-row within the tile
-        const int cchunk = (sizeof(T) == 2) ? (pos ^ (mc_swz(krl, RB / 8) >> 1)) : pos;
+        const int cchunk = (sizeof(T) == 2) ? (pos ^ (mc_swz(krl, RB / 8) >> 1))
+                         : (sizeof(T) == 1) ? (pos ^ mc_swz8(krl)) : pos;
         const int col = origin + cchunk * VEC;
         ok[i] = col < lim;
         if (KIND == L_MC_DENSE) {
@@ -299,6 +308,27 @@ __device__ __forceinline__ i32x8 read_frag_f8(const char* lds, int rowbase, int 
   const u32x4 hi = *(const u32x4*)(lds + row * 128 + (((2 * g + 1) ^ (row & 7)) << 4));
   i32x8 r;
   r[0] = lo.x; r[1] = lo.y; r[2] = lo.z; r[3] = lo.w; r[4] = hi.x; r[5] = hi.y; r[6] = hi.z; r[7] = hi.w;
+  return r;
+}
+
+// fp8 MC (k-major [k][128 B] tile, the weight-gradient operands dY and X): the same operand as
+// read_frag_f8 -- lane l supplies column (l & 15) of the 16 at colbase and the 32 k of group
+// g = l >> 4, byte b = k 32g + b -- assembled from four ds_read_b64_tr_b8: in each, the group's
+// lane 2q + p addresses k-row 32g + 8j + q, bytes 8p..8p+7 of the column chunk, and lane i
+// receives column i of those eight k-rows (byte q = k-row q; profiles/r04_tr_b8_probe.txt).
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+__device__ __forceinline__ i32x8 read_frag_f8_mc(const char* lds, int colbase, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 1, pp = i & 1;
+  const int cb = colbase >> 4;
+  i32x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 32 * g + 8 * j + q;
+    const char* a = lds + k * 128 + ((cb ^ mc_swz8(k)) << 4) + 8 * pp;
+    const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(LDS_PTR(i32x2, a));
+    r[2 * j] = v.x;
+    r[2 * j + 1] = v.y;
+  }
   return r;
 }
 
@@ -493,8 +523,9 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   if (__builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
 #endif
   auto mma_tile = [&](const char* As, const char* Bs) {
-    if constexpr (sizeof(T) == 1) {
-      static_assert(!AMC && !BMC, "fp8 operands are k-contiguous (KC) only");
+    if constexpr (sizeof(T) == 1 && (AMC || BMC)) {
+      return;   // fp8 k-major operands: kstep's own path (read_frag_f8_mc)
+    } else if constexpr (sizeof(T) == 1) {
       i32x8 af[RM], bfr[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i) af[i] = read_frag_f8(As, wm * TM + i * 16, lane);
@@ -567,7 +598,27 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
     constexpr int NXT = (STG + S - 1) % S;
     const char* As = smem + STG * STAGE;
     const char* Bs = As + ABYTES;
-    if constexpr (sizeof(T) == 2 && (AMC || BMC) && (RM + RN) <= 8 && !KSG) {
+    if constexpr (sizeof(T) == 1 && (AMC || BMC)) {
+      // fp8 weight gradient (e5m2 dY x e4m3 X, both k-major): transposed byte reads, so -- as
+      // for bf16 below -- the whole tile's fragments are read before the refill is issued
+      i32x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+        af[i] = AMC ? read_frag_f8_mc(As, wm * TM + i * 16, lane) : read_frag_f8(As, wm * TM + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        bfr[j] = BMC ? read_frag_f8_mc(Bs, wn * TN + j * 16, lane) : read_frag_f8(Bs, wn * TN + j * 16, lane);
+      if (kt + S - 1 < nt) {
+        la.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE, tid);
+        lb.issue(kbeg + (kt + S - 1) * BK, smem + NXT * STAGE + ABYTES, tid);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              af[i], bfr[j], acc[i][j], std::is_same<T, f8e5m2>::value ? 1 : 0, 0, 0, 127, 0, 127);
+    } else if constexpr (sizeof(T) == 2 && (AMC || BMC) && (RM + RN) <= 8 && !KSG) {
       // Transposed (MC) fragments are read with ds_read_b64_tr_b16, which hipcc cannot
       // disambiguate from an in-flight LDS-DMA: a DMA issued before these reads would cost a
       // full vmcnt(0) drain in front of them.  So read the whole tile's fragments FIRST, then
@@ -682,8 +733,13 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   static_assert(!KSG || HR == BM, "KSG sums the two groups' tiles in one staging pass");
   float* cs = (float*)smem;
   float alpha = p.alpha;
-  if (p.scale_a) alpha *= *p.scale_a;
-  if (p.scale_b) alpha *= *p.scale_b;
+  {
+    const float* sa = p.scale_a;
+    const float* sb = p.scale_b;
+    if (p.ngroup && p.grp.SA[batch]) { sa = p.grp.SA[batch]; sb = p.grp.SB[batch]; }
+    if (sa) alpha *= *sa;
+    if (sb) alpha *= *sb;
+  }
   CT* Cb = (p.ngroup ? (CT*)p.grp.C[batch] : (CT*)p.C + (long long)batch * p.c_bs) +
            (p.c_mode == 3 ? (long long)split * p.slab : 0);
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
@@ -1117,6 +1173,14 @@ static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
   return launch_c<T8, CT, 11, LA, L_KC_DENSE>(a, batch, st);
 }
 
+// fp8 weight gradients (e5m2 dY MC_DENSE x e4m3 X MC_DENSE / MC_CONV, fp32 dW or split-K slabs):
+// 128x128 tiles (the MC fp8 reader's 128-byte k-rows), 2- or 3-deep ring (cfg 11 / 13).
+template <int LB>
+static int launch_f8_mc(const GemmArgs& a, int batch, hipStream_t st) {
+  if (a.cfg == 13) return launch_c<f8e5m2, float, 13, L_MC_DENSE, LB>(a, batch, st);
+  return launch_c<f8e5m2, float, 11, L_MC_DENSE, LB>(a, batch, st);
+}
+
 // 32-bit byte-offset limits of the buffer-descriptor loaders (Loader, BUF path)
 static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
   const long long ld = is_a ? a.lda : a.ldb;
@@ -1141,6 +1205,12 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     if (la == L_KC_DENSE) return c_f32 ? launch_f8<float, L_KC_DENSE>(a, batch, st) : launch_f8<bf16, L_KC_DENSE>(a, batch, st);
     if (la == L_KC_CONV) return c_f32 ? launch_f8<float, L_KC_CONV>(a, batch, st) : launch_f8<bf16, L_KC_CONV>(a, batch, st);
     if (la == L_KC_CONV_G) return c_f32 ? launch_f8<float, L_KC_CONV_G>(a, batch, st) : launch_f8<bf16, L_KC_CONV_G>(a, batch, st);
+    return CN_ERR_UNSUPPORTED;
+  }
+  if (dtype == DT_FP8_E5M2 && la == L_MC_DENSE) {   // wgrad: e5m2 dY (k-major) x e4m3 X, fp32 dW
+    if (!c_f32 || a.st_mode || a.row_map || a.c_mode == 1 || a.c_mode == 2) return CN_ERR_UNSUPPORTED;
+    if (lb == L_MC_DENSE) return launch_f8_mc<L_MC_DENSE>(a, batch, st);
+    if (lb == L_MC_CONV) return launch_f8_mc<L_MC_CONV>(a, batch, st);
     return CN_ERR_UNSUPPORTED;
   }
   if (dtype == DT_FP8_E5M2) {   // dgrad: e5m2 output gradients x e4m3 transposed weights, bf16 dX

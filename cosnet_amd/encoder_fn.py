@@ -57,6 +57,14 @@ WGRAD_FLUSH = os.environ.get("CN_WGRAD_FLUSH", "end")
 # over K as well (cn_conv_wgrad_grouped_ws); 0 issues the small ones one by one as split-K
 # launches (A/B runs).
 WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "512"))
+# fp8 mode (configs[4]): the 3x3 bottleneck and ASPP weight gradients on fp8 operands
+# (cn_conv_wgrad_fp8); CN_WGRAD_FP8=0 keeps them bf16 (A/B runs).
+WGRAD_FP8 = os.environ.get("CN_WGRAD_FP8", "1") != "0"
+# TIMING PROBE ONLY (results are wrong): CN_PROBE_SKIP_APPLY=1 / 2 / 3 drops the bn1 / bn2 / both
+# BN + ReLU apply passes of every bottleneck (the next conv reads the raw conv output) -- the
+# upper bound of what folding those applies into the consumer conv's operand path could save
+# (VERDICT r4 "next" #4; profiles/r05_bn_fold_bound.txt).
+_PROBE_SKIP = int(os.environ.get("CN_PROBE_SKIP_APPLY", "0"))
 
 
 def _layer_index(enc):
@@ -79,9 +87,16 @@ class WgradQueue:
     def __init__(self):
         self.jobs = {}
 
-    def add(self, x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None):
+    def add(self, x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None, f8=None):
+        """f8 = (x8, x_state, dy8, dy_state): run this weight gradient on fp8 operands (configs[4],
+        grouped with the other fp8 jobs of its shape; cn_conv_wgrad_fp8)."""
         if dw is None:
             dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=x.device)
+        if f8 is not None:
+            x8, xs, dy8, ds = f8
+            key = ("f8", n, h, w, cin, ops.ld(x8), oh, ow, cout, ops.ld(dy8), k, stride, pad, dil)
+            self.jobs.setdefault(key, []).append((x8, xs, dy8, ds, dw))
+            return dw
         key = (x.dtype, n, h, w, cin, ops.ld(x), oh, ow, cout, ops.ld(dy), k, stride, pad, dil)
         self.jobs.setdefault(key, []).append((x, dy, dw))
         return dw
@@ -89,6 +104,11 @@ class WgradQueue:
     def flush(self):
         for key, jobs in self.jobs.items():
             _, n, h, w, cin, _, oh, ow, cout, _, k, stride, pad, dil = key
+            if key[0] == "f8":
+                for i in range(0, len(jobs), ops.GROUP_MAX):
+                    ops.conv_wgrad_fp8(jobs[i:i + ops.GROUP_MAX], n, h, w, cin, oh, ow, cout, k,
+                                       stride, pad, dil)
+                continue
             # grouped when >= 3 problems give >= 128 workgroups of 128x64 (two layer-4 1x1
             # weight gradients: 2 x 55 us split-K vs 137 us grouped; three: 160 vs 144 us,
             # profiles/r03_wgrad_l4_1x1.txt)
@@ -142,15 +162,20 @@ def fuse_bwd(cin, kdim):
     return kdim >= 1024 and cin <= 256
 
 
-def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=None, weight=None):
+def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=None, weight=None,
+            q8=None):
     """conv -> raw output c and the BN statistics of c per segment.  Train mode: the statistics
     come out of the conv's GEMM epilogue where that is cheaper (ops.conv_fwd_bn, no pass over c),
     else a separate statistics pass; eval: running statistics.  fp8 mode (configs[4]): the
-    conv GEMM takes e4m3 operands (cosnet_amd/fp8.py), statistics by the separate pass."""
+    conv GEMM takes e4m3 operands (cosnet_amd/fp8.py), statistics by the separate pass; with a
+    list q8 the e4m3 input copy is appended to it as Fp8Acts.saved() (for the fp8 weight
+    gradient)."""
     cin = wf.shape[1] // (k * k)
     ctx = getattr(bn, "_cn_fp8", None)
     if weight is not None and ctx is not None and fp8_ok(x, cin) and x.shape[0] > 64:
         x8, xs = ctx.acts.quant(x, id(weight))
+        if q8 is not None:
+            q8.append(ctx.acts.saved(x8, xs))
         wf8, ws = ctx.weights.get(weight)
         c, oh, ow = ops.conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, xs, ws, bias=bias)
         return c, oh, ow, seg_stats(c, bn, training, nseg)
@@ -227,6 +252,28 @@ def fp8_dgrad_ok(dy, k):
             and ops.ld(dy) % 16 == 0 and dy.shape[0] > 64)
 
 
+def wgrad_f8(ctx, q8, dy, rows, k, weight, cin):
+    """fp8 operands for a weight gradient (configs[4]) when both exist: the forward's e4m3 input
+    copy (q8 = Fp8Acts.saved(), frame-a `rows`) and an e5m2 output gradient the fp8 dgrad quantises
+    (fp8_dgrad_ok; the same pass-cached copy serves both).  (x8, x_state, dy8, dy_state) or None."""
+    if ctx is None or not q8 or not fp8_dgrad_ok(dy, k) or cin % 16:
+        return None
+    x8, handle, slot = q8[0]
+    dy8, ds = ctx.grads.quant(dy, ("dgrad", id(weight)))
+    return x8[:rows], handle.state(slot), dy8, ds
+
+
+def wgrad_now(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=None, f8=None):
+    """One weight gradient issued now: fp8 (f8 from wgrad_f8) or the bf16 / fp32 path."""
+    if f8 is None:
+        return conv_wgrad(x, n, h, w, cin, dy, oh, ow, cout, k, stride, pad, dil, dw=dw)
+    if dw is None:
+        dw = torch.empty((cout, k * k * cin), dtype=torch.float32, device=dy.device)
+    x8, xs, dy8, ds = f8
+    ops.conv_wgrad_fp8([(x8, xs, dy8, ds, dw)], n, h, w, cin, oh, ow, cout, k, stride, pad, dil)
+    return dw
+
+
 def dgrad(dy, n, oh, ow, wt, cin, k, pad, dil, h, w, weight, ctx, out=None, accumulate=False):
     """Stride-1 conv dgrad: in fp8 mode (ctx, BASELINE configs[4]) e5m2 output gradients
     (delayed scaling, ctx.grads) x the e4m3 transposed weight on the block-scaled MFMA."""
@@ -267,10 +314,11 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     w3f, w3t = WCACHE.get(blk.conv3.weight, dt)
     c1, oh, ow, st1 = conv_bn(x, n, h, w, w1f, planes, 1, s, 0, 1, blk.bn1, tr, nseg,
                               weight=blk.conv1.weight)
-    y1 = seg_apply(c1, st1, blk.bn1, act=1, fp8_key=id(blk.conv2.weight))
+    y1 = c1 if _PROBE_SKIP & 1 else seg_apply(c1, st1, blk.bn1, act=1, fp8_key=id(blk.conv2.weight))
+    q2 = [] if rec is not None else None
     c2, _, _, st2 = conv_bn(y1, n, oh, ow, w2f, planes, 3, 1, d, d, blk.bn2, tr, nseg,
-                            weight=blk.conv2.weight)
-    y2 = seg_apply(c2, st2, blk.bn2, act=1, fp8_key=id(blk.conv3.weight))
+                            weight=blk.conv2.weight, q8=q2)
+    y2 = c2 if _PROBE_SKIP & 2 else seg_apply(c2, st2, blk.bn2, act=1, fp8_key=id(blk.conv3.weight))
     c3, _, _, st3 = conv_bn(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1, blk.bn3, tr, nseg,
                             weight=blk.conv3.weight)
     cd = std = wdt = None
@@ -287,7 +335,7 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     else:
         y = seg_apply(c3, st3, blk.bn3, act=1, res=x, fp8_key=("out", id(blk)), mask=mk)
     if rec is not None:
-        rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt),
+        rec.append(("block", blk, (x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt, q2),
                     (n // nseg, h, w, oh, ow, s, d, planes, x.shape[1])))
     return y, (n, oh, ow)
 
@@ -297,7 +345,7 @@ def bottleneck_bwd(item, dy, grads, need_dx=True, wq=None):
     dW buffers are registered in `grads` now and filled by wq.flush())."""
     _, blk, sv, (n, h, w, oh, ow, s, d, planes, cin) = item
     wgrad = conv_wgrad if wq is None else wq.add
-    x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt = sv
+    x, c1, y1, c2, y2, c3, cd, mk, st1, st2, st3, std, w1t, w2t, w3t, wdt, q2 = sv
     pi, po = n * h * w, n * oh * ow                     # frame-a rows in / out
     x, c1, y1, c2, y2, c3, mk = x[:pi], c1[:po], y1[:po], c2[:po], y2[:po], c3[:po], mk[:po]
     has_down = cd is not None
@@ -317,8 +365,11 @@ def bottleneck_bwd(item, dy, grads, need_dx=True, wq=None):
     f8 = getattr(blk.bn2, "_cn_fp8", None)
     dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads,
                                  weight=blk.conv3.weight, ctx=f8)
-    dw2 = wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
-                dw=grads.buf(blk.conv2.weight, planes, 9 * planes))
+    # configs[4]: e5m2 dc2 (shared with conv2's fp8 dgrad below) x the forward's e4m3 y1
+    w8 = wgrad_f8(f8, q2, dc2, po, 3, blk.conv2.weight, planes) if WGRAD_FP8 else None
+    dw2 = (wgrad if wq is not None else wgrad_now)(
+        y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d,
+        dw=grads.buf(blk.conv2.weight, planes, 9 * planes), f8=w8)
     dc1, dg1, db1 = dgrad_bn_bwd(dc2, n, oh, ow, w2t, planes, 3, d, d, c1, st1[0], blk.bn1, grads,
                                  weight=blk.conv2.weight, ctx=f8)
     dw1 = wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1,
@@ -368,11 +419,13 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     convs = [(mod.conv2d_0, mod.bn_0, 1, 0)] + [
         (getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)), 3, dd)
         for i, dd in enumerate(mod.cn_dilations)]
-    cs, sts, wts = [], [], []
+    cs, sts, wts, q8s = [], [], [], []
     for bi, (cm, bnm, k, dd) in enumerate(convs):
         wf, wt = WCACHE.get(cm.weight, dt)
+        q = [] if rec is not None else None
         ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias,
-                               weight=cm.weight)
+                               weight=cm.weight, q8=q)
+        q8s.append(q)
         sl = slice(512 * (bi + 1), 512 * (bi + 2))
         if cat8 is not None:
             bn_apply(ci, (st.mean, st.invstd), bnm, act=1, out=cat[:, sl], nseg=st.nseg,
@@ -387,20 +440,23 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     elif ctx is not None:
         ctx.acts.quant(cat, ("cat", id(mod)))   # first use: calibrates the concat's scale
     wbf, wbt = WCACHE.get(mod.bottleneck.weight, dt)
+    qb = [] if rec is not None else None
     cb, _, _, stb = conv_bn(cat, n, h, w, wbf, 256, 3, 1, 1, 1, mod.bn, tr, nseg, bias=mod.bottleneck.bias,
-                            weight=mod.bottleneck.weight)
+                            weight=mod.bottleneck.weight, q8=qb)
     out = seg_apply(cb, stb, mod.bn, act=2, prelu=mod.prelu.weight)
     if rec is not None:
-        rec.append(("aspp", mod, (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out),
+        rec.append(("aspp", mod, (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, q8s, qb),
                     (n // nseg, h, w, [(k, dd) for (_, _, k, dd) in convs])))
     return out
 
 
 def aspp_bwd(item, dout, grads):
     _, mod, sv, (n, h, w, kd) = item
-    x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out = sv
+    x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, q8s, qb = sv
     hw = h * w
     P = n * hw
+    f8 = getattr(mod.bn, "_cn_fp8", None)
+    use8 = f8 is not None and WGRAD_FP8
     x, cat, cb, out = x[:P], cat[:P], cb[:P], out[:P]
     pool, cp, yp = pool[:n], cp[:n], yp[:n]
     pw = mod.prelu.weight
@@ -408,11 +464,12 @@ def aspp_bwd(item, dout, grads):
                                 dgamma=grads.buf(mod.bn.weight, 256), dbeta=grads.buf(mod.bn.bias, 256),
                                 dprelu=grads.buf(pw, 1))
     grads[mod.bottleneck.weight] = as_param_grad(
-        conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1,
-                   dw=grads.buf(mod.bottleneck.weight, 256, 9 * 2560)), mod.bottleneck.weight)
+        wgrad_now(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1,
+                  dw=grads.buf(mod.bottleneck.weight, 256, 9 * 2560),
+                  f8=wgrad_f8(f8, qb, dcb, P, 3, mod.bottleneck.weight, 2560) if use8 else None),
+        mod.bottleneck.weight)
     grads[mod.bottleneck.bias] = ops.colsum(dcb, out=grads.buf(mod.bottleneck.bias, 256))
     grads[mod.bn.weight], grads[mod.bn.bias], grads[pw] = dgb, dbb, dpr
-    f8 = getattr(mod.bn, "_cn_fp8", None)
     dcat = dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, h, w, mod.bottleneck.weight, f8)
     dx = None
     bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
@@ -422,8 +479,10 @@ def aspp_bwd(item, dout, grads):
         dci, dgi, dbi, _ = bn_bwd(ci[:P], dcat[:, sl], None, st[0], bns[bi], act=1,
                                   dgamma=grads.buf(bns[bi].weight, 512), dbeta=grads.buf(bns[bi].bias, 512))
         grads[cms[bi].weight] = as_param_grad(
-            conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1),
-                       dw=grads.buf(cms[bi].weight, 512, k * k * 2048)), cms[bi].weight)
+            wgrad_now(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1),
+                      dw=grads.buf(cms[bi].weight, 512, k * k * 2048),
+                      f8=wgrad_f8(f8, q8s[bi], dci, P, k, cms[bi].weight, 2048) if use8 else None),
+            cms[bi].weight)
         grads[cms[bi].bias] = ops.colsum(dci, out=grads.buf(cms[bi].bias, 512))
         grads[bns[bi].weight], grads[bns[bi].bias] = dgi, dbi
         dx = dgrad(dci, n, h, w, wt, 2048, k, dd, max(dd, 1), h, w, cms[bi].weight, f8, out=dx,

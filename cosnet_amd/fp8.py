@@ -18,7 +18,12 @@ bf16 path.
   the usual gradient format) with delayed scaling of its own (Fp8Context.grads, updated once
   per encoder backward), and multiplied with an e4m3 copy of the transposed weight (current
   scaling, refreshed with the forward copies after every SGD step) -- cn_conv_dgrad_fp8, the
-  block-scaled MFMA with A format e5m2.  Weight gradients stay bf16 x bf16.
+  block-scaled MFMA with A format e5m2.
+* Weight gradients of the same convs (round 5): the e5m2 output gradient above times the e4m3
+  input copy the forward conv read (kept for the backward with the scale it was quantised with:
+  Fp8Acts.end() snapshots the pass's scales before advancing them) -- cn_conv_wgrad_fp8, both
+  operands k-major through ds_read_b64_tr_b8; the bottlenecks' 3x3 convs grouped per layer like
+  the bf16 ones.  The 1x1 / shallow weight gradients (no e5m2 dY) stay bf16 x bf16.
 """
 import struct
 import weakref
@@ -154,9 +159,20 @@ class Fp8Acts:
         self.slots = {}
         self.calibrated = set()
         self.pass_cache = {}
+        self.handle = None
+
+    def slot_of(self, st):
+        """Slot index of a state view returned by state() / quant()."""
+        return (st.data_ptr() - self.states.data_ptr()) // (4 * self.states.element_size())
+
+    def saved(self, x8, st):
+        """(x8, pass handle, slot): what a backward needs to dequantise x8 after end() advanced
+        the live scale -- the handle's snapshot holds the scale x8 was quantised with."""
+        return (x8, self.handle, self.slot_of(st))
 
     def begin(self):
         self.pass_cache = {}
+        self.handle = PassScales()
 
     def state(self, key, device):
         if self.states is None:
@@ -198,10 +214,26 @@ class Fp8Acts:
         self.pass_cache[(x.data_ptr(), tuple(x.shape), ops.ld(x))] = (x8, st, x)
 
     def end(self):
-        """Advance every used scale from the amax collected in this pass (one launch)."""
+        """Advance every used scale from the amax collected in this pass (one launch).  The
+        scales this pass quantised with are kept first (one copy into the pass handle): the fp8
+        weight gradients of the backward read the e4m3 activation copies of this forward."""
         self.pass_cache = {}
         if self.slots:
+            if self.handle is not None:
+                self.handle.snap = self.states[:len(self.slots)].clone()
             ops.fp8_update(self.states[:len(self.slots)])
+
+
+class PassScales:
+    """The scale states of one forward pass as they were while it quantised (Fp8Acts.end())."""
+
+    def __init__(self):
+        self.snap = None
+
+    def state(self, slot):
+        if self.snap is None:
+            raise RuntimeError("fp8 pass scales read before the pass ended")
+        return self.snap[slot]
 
 
 class Fp8Context:

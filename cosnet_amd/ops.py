@@ -390,6 +390,37 @@ def conv_wgrad_grouped(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil, sp
     return [dw for _, _, dw in jobs]
 
 
+def conv_wgrad_fp8(jobs, n, h, w, cin, oh, ow, cout, k, stride, pad, dil):
+    """fp8 weight gradients of G <= GROUP_MAX convs of ONE shape in one launch (cn_conv_wgrad_fp8,
+    BASELINE configs[4]): jobs = [(x8, x_state, dy8, dy_state, dw)] with x8 e4m3 [n*h*w, cin] (the
+    fp8 forward conv's input copy), dy8 e5m2 [n*oh*ow, cout] (the fp8 dgrad's output-gradient
+    copy), their [4]-float scale states (element 0 = dequantisation scale) and dw fp32
+    [cout, k*k*cin] (written).  Split over K into slabs + one reduce launch when small."""
+    import ctypes
+    g = len(jobs)
+    if not 1 <= g <= GROUP_MAX:
+        raise ValueError("1..%d problems per grouped launch" % GROUP_MAX)
+    x0, _, d0, _, _ = jobs[0]
+    if any(ld(x) != ld(x0) or ld(dy) != ld(d0) for x, _, dy, _, _ in jobs):
+        raise ValueError("grouped weight gradients need equal row strides")
+    arr = lambda vals: (ctypes.c_void_p * g)(*vals)
+    xs = arr([j[0].data_ptr() for j in jobs])
+    xst = arr([j[1].data_ptr() for j in jobs])
+    dys = arr([j[2].data_ptr() for j in jobs])
+    dst = arr([j[3].data_ptr() for j in jobs])
+    dws = arr([j[4].data_ptr() for j in jobs])
+    fl = 2.0 * n * oh * ow * cout * k * k * cin
+    ev = _prof_start(g * fl, ("wgrad8", cout, k * k * cin, n * oh * ow),
+                     g * ((n * h * w * cin + n * oh * ow * cout) + 4 * cout * k * k * cin))
+    nws = int(nv.query("cn_conv_wgrad_fp8_workspace_floats", g, n, oh, ow, cout, k, k, cin))
+    ws = torch.empty((nws,), dtype=torch.float32, device=x0.device) if nws else None
+    nv.call("cn_conv_wgrad_fp8", g, ctypes.addressof(xs), ld(x0), n, h, w, cin, ctypes.addressof(dys),
+            ld(d0), oh, ow, cout, k, k, stride, pad, dil, ctypes.addressof(dws), ctypes.addressof(xst),
+            ctypes.addressof(dst), nv.ptr(ws), nws, nv.stream())
+    _prof_end(ev)
+    return [j[4] for j in jobs]
+
+
 def as_param_grad(dw_flat, weight):
     """[cout, k*k*cin] fp32 (OHWI order) -> gradient shaped/stided like the channels_last param."""
     if weight.dim() == 2:

@@ -114,6 +114,20 @@ int cn_conv_dgrad_fp8(const void* dy8, long long lddy, int N, int OH, int OW, in
                       const void* wt8, int Cin, int KH, int KW, int pad, int dil, void* dx,
                       long long lddx, int H, int W, int accumulate, const float* dy_state,
                       const float* w_state, hipStream_t stream);
+
+/* fp8 weight gradients (BASELINE configs[4]): for each of G convs of one shape (G <= 24),
+ * dws[g] (fp32 [Cout][KH][KW][Cin], written) = sum over the N*OH*OW output pixels of
+ * dys8[g] (e5m2 [P][Cout], row stride lddy; the fp8 dgrad's operand) x im2col(xs8[g]) (e4m3
+ * [N*H*W][Cin], row stride ldx; the fp8 forward conv's operand), times the dequantisation scales
+ * dy_states[g][0] * x_states[g][0].  Replaces the weight gradient of conv2d's backward
+ * (deeplab/residual_net.py:59-67 conv2 of Bottleneck, deeplab/deeplabv3_encoder.py:22-31 the ASPP
+ * convs).  ws: cn_conv_wgrad_fp8_workspace_floats floats (split-K slabs; 0 = none needed). */
+size_t cn_conv_wgrad_fp8_workspace_floats(int G, int N, int OH, int OW, int Cout, int KH, int KW, int Cin);
+int cn_conv_wgrad_fp8(int G, const void* const* xs8, long long ldx, int N, int H, int W, int Cin,
+                      const void* const* dys8, long long lddy, int OH, int OW, int Cout, int KH,
+                      int KW, int stride, int pad, int dil, float* const* dws,
+                      const float* const* x_states, const float* const* dy_states, float* ws,
+                      size_t ws_floats, hipStream_t stream);
 /* y (bf16) = conv2d(x8, w8) * x_state[0] * w_state[0] + bias: the fp8 implicit-GEMM conv
  * (block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales).  Cin % 16 == 0. */
 int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin, const void* w8,

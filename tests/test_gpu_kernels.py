@@ -830,6 +830,49 @@ def test_conv_dgrad_fp8(cuda, case, accumulate):
     assert err <= 1e-2, err
 
 
+@pytest.mark.parametrize("case", [
+    # n, cin, h, w, cout, k, stride, pad, dil  (cin, cout % 16; partial M, N and K tiles)
+    (2, 256, 13, 11, 128, 3, 1, 2, 2),     # layer-3-like 3x3 dilated, split over K
+    (2, 64, 30, 30, 256, 3, 1, 1, 1),      # many pixels: several K tiles per split
+    (1, 512, 9, 9, 256, 3, 1, 1, 1),       # the ASPP bottleneck shape class
+    (2, 128, 15, 9, 64, 1, 1, 0, 1),       # 1x1 (dense k-major B operand)
+    (2, 96, 17, 19, 48, 3, 2, 1, 1),       # stride 2
+])
+@pytest.mark.parametrize("G", [1, 3])
+def test_conv_wgrad_fp8(cuda, case, G):
+    """cn_conv_wgrad_fp8 (configs[4] weight gradients: e5m2 dY x e4m3 X, both k-major, through
+    the transposed byte reads ds_read_b64_tr_b8) against fp64 conv2d weight gradients of the
+    exactly-decoded operands times their scales; G problems of one shape per launch, each with its
+    own scales; deterministic (split-K slabs summed in a fixed order).  Only fp32 accumulation
+    remains: 2e-3 of the output scale."""
+    n, cin, h, w, cout, k, s, p, d = case
+    oh, ow = ops.out_hw(h, w, k, s, p, d)
+    jobs, refs = [], []
+    for g in range(G):
+        x = rnd((n, cin, h, w), torch.float32, 90 + g)
+        gy = rnd((n, cout, oh, ow), torch.float32, 95 + g, scale=1e-2 * (g + 1))
+        xs, ds = ops.fp8_state(cuda), ops.fp8_state(cuda, ops.FP8_E5M2)
+        x8 = ops.fp8_quant(nhwc(x).float().to(cuda).contiguous(), xs, ops.FP8_CURRENT)
+        dy8 = ops.fp8_quant(nhwc(gy).float().to(cuda).contiguous(), ds, ops.FP8_CURRENT, fmt=ops.FP8_E5M2)
+        xq = nchw(_dec_e4m3(x8), n, h, w) * xs[0].double().cpu()
+        gq = nchw(_dec_e5m2(dy8), n, oh, ow) * ds[0].double().cpu()
+        wr = torch.zeros((cout, cin, k, k), dtype=torch.float64, requires_grad=True)
+        F.conv2d(xq, wr, None, s, p, d).backward(gq)
+        refs.append(wr.grad)
+        dw = torch.full((cout, k * k * cin), float("nan"), dtype=torch.float32, device=cuda)
+        jobs.append((x8, xs, dy8, ds, dw))
+    ops.conv_wgrad_fp8(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d)
+    first = [j[4].clone() for j in jobs]
+    ops.conv_wgrad_fp8(jobs, n, h, w, cin, oh, ow, cout, k, s, p, d)
+    torch.cuda.synchronize()
+    wp = torch.empty((cout, cin, k, k), device=cuda).contiguous(memory_format=torch.channels_last)
+    for j, f, ref in zip(jobs, first, refs):
+        got = ops.as_param_grad(j[4], wp).double().cpu()
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 2e-3, err
+        assert torch.equal(j[4], f)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("c", [3, 1])
 def test_nchw_to_nhwc(cuda, dt, c):
