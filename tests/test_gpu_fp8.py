@@ -110,8 +110,7 @@ def test_fp8_weight_gradient_of_bottleneck_matches_its_operands(cuda, monkeypatc
     operands (2e-3 of the max: fp32 accumulation only).  Against fp64 of the SAME backward's bf16
     operands (what the bf16 weight gradient computes) it may differ only by the operand
     quantisation itself -- the distance between the two fp64 references, measured in the test
-    (e5m2 keeps 2 mantissa bits: ~0.15 relative L2 on this block), plus the kernel's 2e-3; and the
-    bf16 path's own result (a second pass, CN_WGRAD_FP8 off) sits within that distance too."""
+    (e5m2 keeps 2 mantissa bits: 0.073 relative L2 on this block), plus the kernel's 2e-3."""
     from cosnet_amd import encoder_fn as E
     n1, h, w = 4, 60, 60
     m = C.build_model(torch.bfloat16)
@@ -124,45 +123,39 @@ def test_fp8_weight_gradient_of_bottleneck_matches_its_operands(cuda, monkeypatc
     g = torch.Generator().manual_seed(21)
     x = torch.relu(torch.randn((2 * n1 * h * w, 1024), generator=g)).to(torch.bfloat16).to(cuda)
     dy = (torch.randn((n1 * h * w, 1024), generator=g) * 0.1).to(torch.bfloat16).to(cuda)
-    out = {}
-    for on in (True, False):
-        monkeypatch.setattr(E, "WGRAD_FP8", on)
-        ctx.acts.begin()
-        rec = []
-        E.bottleneck_fwd(blk, x, (2 * n1, h, w), 2, rec)
-        ctx.acts.end()
-        ctx.grads.begin()
-        grads, wq = E.GradSink(), E.WgradQueue()
-        E.bottleneck_bwd(rec[0], dy, grads, wq=wq)
-        wq.flush()
-        torch.cuda.synchronize()
-        dw2 = grads[blk.conv2.weight].detach().double().cpu()
-        if on:
-            q2 = rec[0][2][16]
-            x8, handle, slot = q2[0]
-            sx = handle.state(slot)[0].item()
-            dys = [v for v in ctx.grads.pass_cache.values() if tuple(v[0].shape) == (n1 * h * w, 256)]
-            assert len(dys) == 1, [tuple(v[0].shape) for v in ctx.grads.pass_cache.values()]
-            dy8, ds = dys[0][0], dys[0][1][0].item()
-            def wgrad64(xa, da):
-                xp = torch.nn.functional.pad(xa, (0, 0, 2, 2, 2, 2))
-                ref = torch.empty((256, 256, 3, 3), dtype=torch.float64)
-                for r in range(3):
-                    for s in range(3):
-                        ref[:, :, r, s] = da.t() @ xp[:, 2 * r:2 * r + h, 2 * s:2 * s + w, :].reshape(-1, 256)
-                return ref
-            ref = wgrad64(x8[:n1 * h * w].cpu().view(torch.float8_e4m3fn).double().view(n1, h, w, 256) * sx,
-                          dy8.cpu().view(torch.float8_e5m2).double().view(n1 * h * w, 256) * ds)
-            err = ((dw2 - ref).abs().max() / ref.abs().max()).item()
-            assert err <= 2e-3, err
-            # the same backward's bf16 operands: y1 (frame a) and dc2 (the tensor dy8 quantises)
-            y1 = rec[0][2][2][:n1 * h * w]
-            ref16 = wgrad64(y1.double().cpu().view(n1, h, w, 256), dys[0][2].double().cpu())
-            qerr = ((ref - ref16).norm() / ref16.norm()).item()
-            assert qerr <= 0.25, qerr
-            e16 = ((dw2 - ref16).norm() / ref16.norm()).item()
-            assert e16 <= qerr + 2e-3, (e16, qerr)
-        out[on] = dw2
-        ctx.grads.end()
-    e = ((out[True] - out[False]).norm() / out[False].norm()).item()
-    assert 0 < e <= 1.25 * qerr + 2e-2, (e, qerr)
+    monkeypatch.setattr(E, "WGRAD_FP8", True)
+    ctx.acts.begin()
+    rec = []
+    E.bottleneck_fwd(blk, x, (2 * n1, h, w), 2, rec)
+    ctx.acts.end()
+    ctx.grads.begin()
+    grads, wq = E.GradSink(), E.WgradQueue()
+    E.bottleneck_bwd(rec[0], dy, grads, wq=wq)
+    wq.flush()
+    torch.cuda.synchronize()
+    dw2 = grads[blk.conv2.weight].detach().double().cpu()
+    x8, handle, slot = rec[0][2][16][0]          # conv2's saved e4m3 input (Fp8Acts.saved)
+    sx = handle.state(slot)[0].item()
+    dys = [v for v in ctx.grads.pass_cache.values() if tuple(v[0].shape) == (n1 * h * w, 256)]
+    assert len(dys) == 1, [tuple(v[0].shape) for v in ctx.grads.pass_cache.values()]
+    dy8, ds = dys[0][0], dys[0][1][0].item()
+
+    def wgrad64(xa, da):
+        xp = torch.nn.functional.pad(xa, (0, 0, 2, 2, 2, 2))
+        ref = torch.empty((256, 256, 3, 3), dtype=torch.float64)
+        for r in range(3):
+            for s in range(3):
+                ref[:, :, r, s] = da.t() @ xp[:, 2 * r:2 * r + h, 2 * s:2 * s + w, :].reshape(-1, 256)
+        return ref
+    ref = wgrad64(x8[:n1 * h * w].cpu().view(torch.float8_e4m3fn).double().view(n1, h, w, 256) * sx,
+                  dy8.cpu().view(torch.float8_e5m2).double().view(n1 * h * w, 256) * ds)
+    err = ((dw2 - ref).abs().max() / ref.abs().max()).item()
+    assert err <= 2e-3, err
+    # the same backward's bf16 operands: y1 (frame a) and dc2 (the tensor dy8 quantises)
+    y1 = rec[0][2][2][:n1 * h * w]
+    ref16 = wgrad64(y1.double().cpu().view(n1, h, w, 256), dys[0][2].double().cpu())
+    qerr = ((ref - ref16).norm() / ref16.norm()).item()
+    assert 0 < qerr <= 0.15, qerr
+    e16 = ((dw2 - ref16).norm() / ref16.norm()).item()
+    assert e16 <= qerr + 2e-3, (e16, qerr)
+    ctx.grads.end()

@@ -10,4 +10,4 @@ timeout -k 10 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $CMD > $OUT/fetch.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $CMD > $OUT/write.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/mfma -o run -- $CMD > $OUT/mfma.log 2>&1
-python3 tools/pmc_summary.py $OUT/fetch $OUT/write $OUT/mfma > $OUT/summary.json
+python3 tools/pmc_summary.py --steps 2 $OUT/fetch $OUT/write $OUT/mfma > $OUT/summary.json
