@@ -142,7 +142,7 @@ def load():
 
 
 HASHED_SOURCES = ["gemm.hip", "conv.hip", "bn.hip", "ew.hip", "coatt.hip", "coatt_fused.hip",
-                  "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip",
+                  "coatt_q48.hip", "coatt_flash.hip", "coatt_f8.hip", "fp8.hip", "frames.hip", "eval.hip",
                   "common.h", "gemm.h", "coatt_fused.h", "../../include/cosnet_hip.h"]   # csrc/Makefile HASHED, same order
 
 

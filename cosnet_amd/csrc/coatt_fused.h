@@ -29,7 +29,19 @@ struct FusedArgs {
   int nitems, nfull, nsplit, tps;
   float* opart;    // [nsplit][nitems - nfull][128][256]
   float* mlpart;   // [nsplit][nitems - nfull][128][2]
+  // coatt_q48_k (stream-K): key tiles per item, partial slots per item, per-item arrival counters
+  int ntiles, smax;
+  int* cnt;
 };
 
 // coatt_dsplit.hip: the d-split wave-pair variant (kernel variant 4) of the forward / PV kernel
 int coatt_dsplit_launch(int mode, const FusedArgs& a, dim3 grid, hipStream_t st);
+
+// coatt_q48.hip: 48 query rows per wave on 16x16x32 MFMA tiles (kernel variant 5), 192-row items,
+// stream-K work split.  coatt_q48_launch takes a.dir / HW / HWp / accumulate; with a workspace of
+// coatt_q48_workspace_bytes (and merge_ok: 16-byte output rows) it cuts items across 256
+// workgroups, else it runs one workgroup per item.
+int coatt_q48_rows();
+size_t coatt_q48_workspace_bytes(int items, int ntiles);
+int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void* ws,
+                     size_t ws_bytes, hipStream_t st);

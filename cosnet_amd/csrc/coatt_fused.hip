@@ -1036,28 +1036,37 @@ static void plan_split(int items, int ntiles, int* nfull, int* nsplit) {
   *nsplit = s;
 }
 
-// Kernel variant: 1 = coatt_fused_fwd_k (4 waves, one per SIMD), 2 = coatt_fused2_k (wave pairs,
-// duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys), 4 = coatt_dsplit_k
-// (coatt_dsplit.hip: wave pairs splitting the channels, 64 query rows per pair).  CN_COATT_VARIANT picks the
-// default; cn_coatt_force_variant overrides it (tests, A/B tools).
+// Kernel variant: 1 = coatt_fused_fwd_k (4 waves, one per SIMD, 32 rows per wave), 2 =
+// coatt_fused2_k (wave pairs, duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys),
+// 4 = coatt_dsplit_k (coatt_dsplit.hip: wave pairs splitting the channels, 64 query rows per
+// pair), 5 = coatt_q48_k (coatt_q48.hip: 48 rows per wave, Q in registers, 16x16x32 tiles).
+// CN_COATT_VARIANT picks the default; cn_coatt_force_variant overrides it (tests, A/B tools).
 static int g_coatt_variant = 0;
+static bool variant_built(int x) { return x == 1 || x == 5 || (CN_EXPERIMENTAL && x >= 2 && x <= 4); }
 static int coatt_variant() {
   static const int v = [] {
     const char* e = getenv("CN_COATT_VARIANT");
     const int x = e ? atoi(e) : 1;
-    return (x >= 1 && x <= (CN_EXPERIMENTAL ? 4 : 1)) ? x : 1;
+    return variant_built(x) ? x : 1;
   }();
   return g_coatt_variant ? g_coatt_variant : v;
 }
 
-// Development / test hook: force the forward / PV kernel variant (1..4 as above; 0: default).
+// Development / test hook: force the forward / PV kernel variant (1..5 as above; 0: default).
 // Returns the previous setting.
 // Variants 2-4 exist only in CN_EXPERIMENTAL builds (-1 otherwise, nothing changed).
 extern "C" int cn_coatt_force_variant(int v) {
-  if (!CN_EXPERIMENTAL && v >= 2 && v <= 4) return -1;
+  if (v != 0 && !variant_built(v)) return -1;
   const int old = g_coatt_variant;
-  g_coatt_variant = (v >= 1 && v <= 4) ? v : 0;
+  g_coatt_variant = v;
   return old;
+}
+
+// The variant-5 launch of one co-attention call (coatt_q48.hip): work cut across the CUs when the
+// outputs take the merge's 16-byte rows (merge_ok) and the workspace holds the partials.
+static int q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void* ws,
+                      size_t ws_bytes, hipStream_t st) {
+  return coatt_q48_launch(mode, a, B, nd, merge_ok, ws, ws_bytes, st);
 }
 
 static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
@@ -1100,6 +1109,10 @@ static int fused_launch(int mode, FusedArgs& a, int B, int nd, hipStream_t st) {
 }
 
 extern "C" size_t cn_coatt_fused_workspace_bytes(int B, int HW, int ndir) {
+  if (coatt_variant() == 5) {
+    const int rb = coatt_q48_rows();
+    return coatt_q48_workspace_bytes((HW + rb - 1) / rb * B * ndir, (HW + FBK - 1) / FBK);
+  }
   const int nrb = (HW + FBQ - 1) / FBQ;
   int nfull, s;
   plan_split(nrb * B * ndir, (HW + FBK - 1) / FBK, &nfull, &s);
@@ -1137,10 +1150,12 @@ extern "C" int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const vo
   if (nd == 0) return CN_ERR_SHAPE;
   a.HW = HW;
   a.HWp = (HW + 31) / 32 * 32;
+  // the merge writes 16-byte rows: unsplit when the outputs are not laid out for that
+  const bool merge_ok = !(((uintptr_t)za & 15) || ((uintptr_t)zb & 15) || (ld_z % 8));
+  if (coatt_variant() == 5) return q48_launch(0, a, B, nd, merge_ok, ws, ws_bytes, st);
   const int nrb = (HW + FBQ - 1) / FBQ;
   plan_split(nrb * B * nd, (HW + FBK - 1) / FBK, &a.nfull, &a.nsplit);
-  // the merge writes 16-byte rows: unsplit when the outputs are not laid out for that
-  if (((uintptr_t)za & 15) || ((uintptr_t)zb & 15) || (ld_z % 8)) a.nsplit = 1;
+  if (!merge_ok) a.nsplit = 1;
   if (a.nsplit > 1) {
     const size_t tail_rows = (size_t)a.nsplit * (nrb * B * nd - a.nfull) * FBQ;
     // no (or a too small / misaligned) workspace: the unsplit launch, as the _ws siblings do
@@ -1172,6 +1187,7 @@ extern "C" int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void*
   a.HW = HW;
   a.HWp = (HW + 31) / 32 * 32;
   a.accumulate = 0;
+  if (coatt_variant() == 5) return q48_launch(0, a, B, nd, false, nullptr, 0, st);
   return fused_launch(0, a, B, nd, st);
 }
 
@@ -1188,9 +1204,11 @@ extern "C" int cn_coatt_flash_pv_ws(const void* q, long long ldq, const void* k,
   a.HW = HW;
   a.HWp = (HW + 31) / 32 * 32;
   a.accumulate = accumulate;
+  const bool merge_ok = !(((uintptr_t)o & 15) || (ldo % 8));
+  if (coatt_variant() == 5) return q48_launch(1, a, B, 1, merge_ok, ws, ws_bytes, st);
   const int nrb = (HW + FBQ - 1) / FBQ;
   plan_split(nrb * B, (HW + FBK - 1) / FBK, &a.nfull, &a.nsplit);
-  if (((uintptr_t)o & 15) || (ldo % 8)) a.nsplit = 1;
+  if (!merge_ok) a.nsplit = 1;
   if (a.nsplit > 1) {
     const size_t tail_rows = (size_t)a.nsplit * (nrb * B - a.nfull) * FBQ;
     if (!ws || ws_bytes < tail_rows * FD * sizeof(float) || !aligned16(ws)) a.nsplit = 1;

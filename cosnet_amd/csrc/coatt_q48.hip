@@ -1,0 +1,551 @@
+// Flash co-attention forward / PV with 48 query rows per wave on 16x16x32 MFMA tiles
+// (kernel variant 5; rgbd_segmentation_RAA.py:160-170, :213-221).
+//
+//   MODE 0:  O[q] = sum_k softmax_k(Q[q].K[k]) V[k]                    (+ log2-sum-exp2 per row)
+//   MODE 1:  O[q] (+)= sum_k exp2(Q[q].K[k] log2e - klse[k]) V[k]      (the backward's P_row dZ_b)
+//
+// The 32-row kernel (coatt_fused_fwd_k) reads, per 32-key tile and wave, the whole K tile, the
+// whole V tile and its 32 Q rows from LDS and issues a quarter of the tile's LDS-DMA pieces for
+// 32 MFMAs of 32x32x16; its measured bounds are exactly those.  A 64-row wave would
+// halve them but does not fit the register file at D = 256 (profiles/r05_coatt_q64_isa.txt).  Here
+// a wave owns 48 query rows = three 16-row tiles, with their Q fragments in REGISTERS (96 VGPRs):
+// every K fragment read feeds three S MFMAs and every V^T fragment three PV MFMAs, no Q is read
+// from LDS, and the tile's DMA pieces are spread over 96 MFMAs (16x16x32) instead of 32 (32x32x16)
+// -- per FLOP a third of the K / V reads and of the DMA issue, no Q reads.  Accumulators: O = 16
+// channel tiles x 3 row tiles x 4 = 192 registers, S^T = 2 key tiles x 3 row tiles x 4 = 24, both
+// within the 256 accumulation registers.
+//
+// Operand maps (16x16x32 bf16 MFMA: A lane l = row (l & 15), k = 8 (l >> 4) + j; B lane l =
+// column (l & 15), same k; C lane l = rows 4 (l >> 4) + i, column l & 15):
+//   S^T[key][q] = K Q^T: A = K (16 keys x 32 channels, a ds_read_b128 of the K image), B = Q.
+//   The S^T accumulators of the tile's two 16-key halves leave lane (q = l & 15, g = l >> 4) the
+//   keys {4g + i, 16 + 4g + i}: packed to bf16 in that order they ARE the B operand of
+//   O^T[d][q] += V^T P^T with k slot 8g + j <-> key (j < 4 ? 4g + j : 16 + 4g + j - 4), and the A
+//   operand V^T takes the same order from two ds_read_b64_tr_b16 (keys 4g..4g+3 and 16+4g..+3,
+//   lane i receiving channel i of the 16-channel tile).
+// Work split (stream-K): 48-row waves leave a 4-wave workgroup 192 query rows, so a 60 x 60 map
+// of 5 pairs x 2 directions is 190 such items -- 74 % of 256 CUs for one round, 59 % at 4 pairs.
+// Instead the items' key tiles are laid end to end (item-major) and cut into nwork equal ranges,
+// one workgroup each (nwork = 256: every CU busy for the same number of tile steps).  A range
+// covering a whole item writes its output directly; a segment of a cut item writes its
+// un-normalised fp32 O and per-row (reference, sum) to the item's partial slot and bumps the
+// item's arrival counter; the LAST segment to arrive (no workgroup ever waits for another, so no
+// co-residency is assumed) merges the item's slots in segment order and writes the output.
+// The merge order is fixed (slots 0, 1, ...), so results do not depend on arrival order.
+// LDS images (one 3-stage ring, 2 x 16 KB per stage) are FRAGMENT-MAJOR: the K image is 16
+// blocks of 1 KB, block (kt, ds) holding at lane slot L the 16 bytes lane L feeds the MFMA
+// (key 16 kt + (L & 15), channels 32 ds + 8 (L >> 4) ..); the V image is 32 blocks of 512 B,
+// block (dt, hi) holding at 8-byte slot L what lane L addresses in its transposed read.  Every
+// fragment read is then one contiguous, conflict-free block at (lane base + immediate offset):
+// no swizzle arithmetic in the loop.  The LDS-DMA fills them with 16-byte chunks gathered from
+// 16 (K) or 32 (V) key rows per 1-KB piece.
+#include "common.h"
+#include "coatt_fused.h"
+#include <algorithm>
+#include <type_traits>
+#include "../../include/cosnet_hip.h"
+
+namespace {
+
+constexpr int RW = 48;                 // query rows per wave (3 tiles of 16)
+constexpr int RB = 4 * RW;             // query rows per workgroup (4 waves)
+constexpr int Q48ST = 3;               // K / V ring stages
+constexpr float Q48_GROWTH = 64.0f;    // allowed growth of a row's maximum over its first tile (log2 units)
+
+__device__ __attribute__((aligned(16))) unsigned g_zero16_q48[4];
+
+__device__ __forceinline__ void glds16r(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void raw_barrier_r() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Partial rows cross workgroups (and XCDs, each with its own L2): written through to memory and
+// read past the L2 (cache policy sc0 sc1, system coherence) instead of device-wide fences, which
+// write back and invalidate the whole L2 -- the K / V stream the XCD's other workgroups share.
+constexpr int CP_SYS = 1 | 16;   // sc0 | sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t part_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ unsigned lds_addr_r(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait_r(bf16x8& v) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(v) : "n"(N));
+}
+
+// The workgroup whose range holds key-tile step u of the item-major list (ranges [w U / G,
+// (w+1) U / G), U = nitems x ntiles, G = nwork): the largest w with floor(w U / G) <= u.
+__device__ __forceinline__ int q48_owner(long long u, long long U, int G) {
+  return (int)(((u + 1) * G + U - 1) / U) - 1;
+}
+
+// One segment: key tiles [tb, tb + nt) of `item`; `slot` < 0: the whole item, output directly,
+// else the partial slot it writes.
+template <int MODE>
+__device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* wg_ovf, int item,
+                                            int tb, int nt, int slot) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const bool part = slot >= 0;
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const int HW = a.HW;
+  const long long b = bd / a.ndir;
+  const bf16* Q = d.q + b * HW * d.ldq;
+  const bf16* K = d.k + b * HW * d.ldk;
+  const bf16* V = d.v + b * HW * d.ldv;
+  const int qw0 = rb * RB + w * RW;          // this wave's first query row
+  const void* zp = (const void*)g_zero16_q48;
+
+  // LDS-DMA: piece i of a tile is, for wave w, K block kb_i = 4 i + w (kt = kb_i >> 3, ds = kb_i & 7)
+  // and V block pair dt = 4 i + w.  A lane's global offset is a tile-invariant per-lane part plus
+  // a uniform part: no per-piece vector address arithmetic.
+  //   K block (kt, ds), lane L = (col = L & 15, g = L >> 4): K[key0 + 16 kt + col][32 ds + 8 g .. +8]
+  //   V pair dt, lane L = (hi = L >> 5, g' = (L >> 3) & 3, q4 = (L >> 1) & 3, jl = L & 1):
+  //     V[key0 + 16 hi + 4 g' + q4][16 dt + 8 jl .. +8]
+  const unsigned ldk2 = (unsigned)d.ldk * 2, ldv2 = (unsigned)d.ldv * 2;
+  const int vkey = 16 * (lane >> 5) + 4 * ((lane >> 3) & 3) + ((lane >> 1) & 3);
+  const unsigned koff = col * ldk2 + g * 16;
+  const unsigned voff = vkey * ldv2 + (lane & 1) * 16;
+  const int wq = __builtin_amdgcn_readfirstlane(w);
+  const int bp16 = (lane ^ 16) << 2, bp32 = (lane ^ 32) << 2;   // ds_bpermute byte addresses
+  auto issue_piece = [&](int t, int stage, int i) {
+    const int kbi = 4 * i + wq;                    // K block index = V block pair index
+    char* kb = lds + stage * 2 * FTILE + kbi * 1024;
+    char* vb = lds + stage * 2 * FTILE + FTILE + kbi * 1024;
+    const int key0 = (tb + t) * FBK;
+    const char* kr = (const char*)K + (long long)(key0 + 16 * (kbi >> 3)) * ldk2 + (kbi & 7) * 64;
+    const char* vr = (const char*)V + (long long)key0 * ldv2 + kbi * 32;
+    if (key0 + FBK <= HW) {
+      glds16r(kr + koff, kb);
+      glds16r(vr + voff, vb);
+    } else {   // the last, partial tile: rows past HW read the zero page
+      const bool okk = key0 + 16 * (kbi >> 3) + col < HW, okv = key0 + vkey < HW;
+      glds16r(okk ? (const void*)(kr + koff) : zp, kb);
+      glds16r(okv ? (const void*)(vr + voff) : zp, vb);
+    }
+  };
+  auto issue = [&](int t, int stage) {
+#pragma unroll
+    for (int i = 0; i < FTILE / 4096; ++i) issue_piece(t, stage, i);
+  };
+
+  // Q fragments (B operand of S^T = K Q^T), straight from global memory, issued before the K / V
+  // prologue (older than every DMA piece, so the loop's counted waits cover them):
+  // qf[qt][ds] = Q[qw0 + 16 qt + col][32 ds + 8 g .. +8]  (rows past HW: zero)
+  bf16x8 qf[3][8];
+#pragma unroll
+  for (int qt = 0; qt < 3; ++qt) {
+    const int row = qw0 + 16 * qt + col;
+    const bf16* qp = Q + (long long)(row < HW ? row : 0) * d.ldq + 8 * g;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) qf[qt][ds] = *(const bf16x8*)(qp + 32 * ds);
+    if (row >= HW) {
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) qf[qt][ds] = bf16x8{};
+    }
+  }
+  f32x4 o[16][3];
+  float m[3] = {-INFINITY, -INFINITY, -INFINITY};
+  float mt[3] = {-INFINITY, -INFINITY, -INFINITY};   // running maxima (pass 0)
+  __attribute__((ext_vector_type(2))) float l[3];   // per-lane partial sums (pairs)
+  bool ovf = false;
+  const float L2E = 1.4426950408889634f;
+
+  // pass 0: reference = each row's maximum over its first tile; pass 1 (only when a row of the
+  // workgroup outgrew its reference by more than Q48_GROWTH): again with the exact maxima
+  auto run = [&](auto passc) {
+  constexpr int pass = decltype(passc)::value;
+  if (pass) {
+#pragma unroll
+    for (int qt = 0; qt < 3; ++qt) m[qt] = mt[qt];
+  }
+#pragma unroll
+  for (int dt = 0; dt < 16; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 3; ++qt) o[dt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int qt = 0; qt < 3; ++qt) l[qt] = 0.f;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+
+  int st = 0, st2 = 2;
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * FTILE / 4096) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_r();
+    const bool dodma = t + 2 < nt;
+    const int dst2 = st2;
+    const char* kb = lds + st * 2 * FTILE;
+    st = st == Q48ST - 1 ? 0 : st + 1;
+    st2 = st2 == Q48ST - 1 ? 0 : st2 + 1;
+    const char* vb = kb + FTILE;
+    const int key0 = (tb + t) * FBK;
+    // the fragment-major images: every fragment read is this lane's slot of one contiguous block
+    const unsigned kla = lds_addr_r(kb) + lane * 16, vla = lds_addr_r(vb) + lane * 8;
+
+    // MODE 1: the per-key normalisers of the lane's 8 keys {4g + i, 16 + 4g + i}
+    f32x4 nk[2];
+    if constexpr (MODE == 1) {
+      const float* kl = d.klse + b * a.HWp + key0 + 4 * g;
+      nk[0] = *(const f32x4*)kl;
+      nk[1] = *(const f32x4*)(kl + 16);
+    }
+    // ---- S^T tiles: s[kt][qt] = K[16 kt .. +16] Q[16 qt .. +16]^T over 8 channel steps of 32
+    f32x4 s[2][3];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 3; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      // K fragment (A): key 16 kt + col, channels 32 ds + 8 g .. +8 = block 8 kt + ds, slot lane
+      auto kread = [&](int kt, int ds) {
+        return *(const bf16x8*)((const __attribute__((address_space(3))) char*)(uintptr_t)kla + (8 * kt + ds) * 1024);
+      };
+      bf16x8 kf[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kf[u] = kread(u & 1, u >> 1);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {          // it = 2 ds + kt
+        const int kt = it & 1, ds = it >> 1;
+        const bf16x8 kc = kf[it & 3];
+        if (it + 4 < 16) kf[it & 3] = kread((it + 4) & 1, (it + 4) >> 1);
+#pragma unroll
+        for (int qt = 0; qt < 3; ++qt)
+          s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kc, qf[qt][ds], s[kt][qt], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        if (it + 4 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+
+    // ---- softmax per row tile: the lane's row q = 16 qt + col, its keys {4g + i, 16 + 4g + i}
+    // (pairs of values in packed fp32 FMAs / adds; the partial last tile's key mask as its own
+    // copy of the code, not selects on every tile)
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    bf16x8 pf[3];
+    auto soft = [&](auto qtc, auto maskc) {
+      constexpr int qt = decltype(qtc)::value;
+      constexpr bool MASK = decltype(maskc)::value;
+      f32x2 v[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        v[i] = f32x2{s[0][qt][2 * i], s[0][qt][2 * i + 1]};
+        v[2 + i] = f32x2{s[1][qt][2 * i], s[1][qt][2 * i + 1]};
+      }
+      const f32x2 l2e = {L2E, L2E};
+      if constexpr (MODE == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 nkp = {nk[i >> 1][2 * (i & 1)], nk[i >> 1][2 * (i & 1) + 1]};
+          v[i] = v[i] * l2e - nkp;
+          v[i] = f32x2{__builtin_amdgcn_exp2f(v[i].x), __builtin_amdgcn_exp2f(v[i].y)};
+        }
+      } else {
+        if constexpr (MASK) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (key0 + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4) >= HW) v[j >> 1][j & 1] = -INFINITY;
+        }
+        float mx = fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
+                         fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
+        mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_ds_bpermute(bp16, __float_as_int(mx))));
+        mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_ds_bpermute(bp32, __float_as_int(mx))));
+        // fixed reference: the row's maximum over its first key tile (O is still zero there, so
+        // nothing is rescaled); later tiles may exceed it by up to Q48_GROWTH (log2 units: P and
+        // the fp32 sums stay far from overflow), beyond that the row is redone (ovf)
+        if constexpr (pass == 0) {
+          if (t == 0) m[qt] = mx * L2E;
+          else ovf |= mx * L2E > m[qt] + Q48_GROWTH;
+          mt[qt] = fmaxf(mt[qt], mx * L2E);
+        }
+        const f32x2 nm = {-m[qt], -m[qt]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = v[i] * l2e + nm;
+          v[i] = f32x2{__builtin_amdgcn_exp2f(v[i].x), __builtin_amdgcn_exp2f(v[i].y)};
+        }
+        l[qt] += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (bf16)v[j >> 1][j & 1];
+      pf[qt] = r;
+    };
+    if (MODE == 0 && key0 + FBK > HW) {
+      soft(std::integral_constant<int, 0>{}, std::true_type{});
+      soft(std::integral_constant<int, 1>{}, std::true_type{});
+      soft(std::integral_constant<int, 2>{}, std::true_type{});
+    } else {
+      soft(std::integral_constant<int, 0>{}, std::false_type{});
+      soft(std::integral_constant<int, 1>{}, std::false_type{});
+      soft(std::integral_constant<int, 2>{}, std::false_type{});
+    }
+
+    // ---- O^T[16 dt .. +16][q] += V^T P^T: the V^T fragment (A) of channel tile dt in the k order
+    // of P: two transposed reads, keys 4g .. 4g+3 and 16 + 4g .. +3; lane 4q4 + p4 of a 16-lane
+    // group addresses key row (base + q4), channels 16 dt + 4 p4 .. +3 (8 bytes)
+    {
+      // block (dt, hi) holds, at lane 16 G + 4 q4 + p4, V[16 hi + 4 G + q4][16 dt + 4 p4 .. +3]
+      auto vread = [&](int dt) {
+        u32x2 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(vla), "n"(dt * 1024));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(vla), "n"(dt * 1024 + 512));
+        u32x4 v = {lo.x, lo.y, hi.x, hi.y};
+        return __builtin_bit_cast(bf16x8, v);
+      };
+      constexpr int VPF = 3;
+      bf16x8 vf[VPF];
+#pragma unroll
+      for (int u = 0; u < VPF; ++u) vf[u] = vread(u);
+#pragma unroll
+      for (int dt = 0; dt < 16; ++dt) {
+        bf16x8 cur = vf[dt % VPF];
+        if (dt + VPF < 16) vf[dt % VPF] = vread(dt + VPF);
+        const int younger = 2 * (15 - dt < VPF ? 15 - dt : VPF);
+        if (younger >= 6) lgkm_wait_r<6>(cur);
+        else if (younger == 4) lgkm_wait_r<4>(cur);
+        else if (younger == 2) lgkm_wait_r<2>(cur);
+        else lgkm_wait_r<0>(cur);
+#pragma unroll
+        for (int qt = 0; qt < 3; ++qt)
+          o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, pf[qt], o[dt][qt], 0, 0, 0);
+        if ((dt & 3) == 3 && dodma) issue_piece(t + 2, dst2, dt >> 2);
+      }
+    }
+  }
+  };
+  run(std::integral_constant<int, 0>{});
+  if constexpr (MODE == 0) {
+    // any overflow in the workgroup?  (the barrier also retires every wave's reads of the ring
+    // before pass 1's DMA refills it)
+    const bool wave_ovf = __builtin_amdgcn_ballot_w64(ovf) != 0;   // all lanes vote
+    if (lane == 0) wg_ovf[w] = wave_ovf;
+    raw_barrier_r();
+    if (wg_ovf[0] | wg_ovf[1] | wg_ovf[2] | wg_ovf[3]) run(std::integral_constant<int, 1>{});
+  }
+
+  // ---- epilogue: o[dt][qt][i] = O^T[16 dt + 4 g + i][16 qt + col]
+#pragma unroll
+  for (int qt = 0; qt < 3; ++qt) {
+    float lt = l[qt].x + l[qt].y;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const int qrow = qw0 + 16 * qt + col;
+    if (part) {
+      if (qrow < HW) {
+        const unsigned prow = (unsigned)slot * RB + (unsigned)(qrow - rb * RB);
+        const __amdgpu_buffer_rsrc_t ro = part_rsrc(a.opart);
+#pragma unroll
+        for (int dt = 0; dt < 16; ++dt)
+          __builtin_amdgcn_raw_buffer_store_b128(o[dt][qt], ro, (prow * FD + 4 * g + 16 * dt) * 4, 0, CP_SYS);
+        if (MODE == 0 && g == 0) {
+          typedef __attribute__((ext_vector_type(2))) float f32x2;
+          __builtin_amdgcn_raw_buffer_store_b64(f32x2{m[qt], lt}, part_rsrc(a.mlpart), prow * 8, 0, CP_SYS);
+        }
+      }
+      continue;
+    }
+    if (MODE == 0 && d.lse && g == 0 && qrow < a.HWp)
+      d.lse[b * a.HWp + qrow] = qrow < HW ? m[qt] + __builtin_amdgcn_logf(lt) : INFINITY;
+    if (qrow < HW) {
+      const float inv = MODE == 0 ? 1.f / lt : 1.f;
+      bf16* op = d.o + (b * HW + qrow) * d.ldo + 4 * g;
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+      for (int dt = 0; dt < 16; ++dt) {
+        bf16x4 v;
+        if (a.accumulate) {
+          const bf16x4 old = *(const bf16x4*)(op + 16 * dt);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][qt][j] * inv + (float)old[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[dt][qt][j] * inv);
+        }
+        *(bf16x4*)(op + 16 * dt) = v;
+      }
+    }
+  }
+}
+
+// Merge of a cut item (by its last-arriving segment): slots slot0 .. slot0 + nseg - 1 in order,
+// an online (max, sum) fold per row.  A thread owns MB (row, 8-channel) chunks at once and issues
+// the loads of one slot for all of them together: nseg x 2 round trips to memory per thread, not
+// one per chunk and slot (the partial rows are read past the L2, ~1-2 us each).
+template <int MODE>
+__device__ __forceinline__ void q48_merge(const FusedArgs& a, int item, int nseg, int slot0) {
+  constexpr int MB = 6;                                   // chunks per thread and batch
+  constexpr int NCH = RB * (FD / 8);                      // 6144 chunks = 4 batches of 256 x 6
+  static_assert(NCH % (256 * MB) == 0, "merge batches");
+  const int rb = item % a.nrb, bd = item / a.nrb;
+  const FusedDir d = a.dir[bd % a.ndir];
+  const long long b = bd / a.ndir;
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  const __amdgpu_buffer_rsrc_t ro = part_rsrc(a.opart), rml = part_rsrc(a.mlpart);
+  for (int base = 0; base < NCH; base += 256 * MB) {
+    float acc[MB][8], M[MB], L[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      M[j] = -INFINITY;
+      L[j] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+    }
+    for (int s = 0; s < nseg; ++s) {
+      f32x4 v0[MB], v1[MB];
+      f32x2 ml[MB];
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        const int idx = base + j * 256 + threadIdx.x;
+        const unsigned prow = (unsigned)(slot0 + s) * RB + idx / (FD / 8);
+        const unsigned off = (prow * FD + (idx % (FD / 8)) * 8) * 4;
+        v0[j] = __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, CP_SYS);
+        v1[j] = __builtin_amdgcn_raw_buffer_load_b128(ro, off + 16, 0, CP_SYS);
+        if constexpr (MODE == 0) ml[j] = __builtin_amdgcn_raw_buffer_load_b64(rml, prow * 8, 0, CP_SYS);
+      }
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        float ws = 1.f, wo = 1.f;
+        if constexpr (MODE == 0) {
+          const float mn = fmaxf(M[j], ml[j].x);
+          wo = __builtin_amdgcn_exp2f(M[j] - mn);          // 0 on the first slot (M = -inf)
+          ws = ml[j].y > 0.f ? __builtin_amdgcn_exp2f(ml[j].x - mn) : 0.f;
+          M[j] = mn;
+          L[j] = fmaf(ml[j].y, ws, L[j] * wo);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[j][e] = fmaf(v0[j][e], ws, acc[j][e] * wo);
+          acc[j][4 + e] = fmaf(v1[j][e], ws, acc[j][4 + e] * wo);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const int idx = base + j * 256 + threadIdx.x;
+      const int row = idx / (FD / 8), c0 = (idx % (FD / 8)) * 8;
+      const int q = rb * RB + row;
+      if (q >= a.HW) {
+        if (MODE == 0 && d.lse && c0 == 0 && q < a.HWp) d.lse[b * a.HWp + q] = INFINITY;
+        continue;
+      }
+      bf16* op = d.o + (b * a.HW + q) * d.ldo + c0;
+      const float inv = MODE == 0 ? 1.f / L[j] : 1.f;
+      bf16x8 outv;
+      if (MODE == 1 && a.accumulate) {
+        const bf16x8 old = *(const bf16x8*)op;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) outv[e] = (bf16)(acc[j][e] + (float)old[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) outv[e] = (bf16)(acc[j][e] * inv);
+      }
+      *(bf16x8*)op = outv;
+      if (MODE == 0 && d.lse && c0 == 0) d.lse[b * a.HWp + q] = M[j] + __builtin_amdgcn_logf(L[j]);
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void coatt_q48_k(FusedArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[Q48ST * 2 * FTILE];   // 96 KB
+  __shared__ int wg_ovf[4];
+  __shared__ int wg_last;
+  const int G = a.nwork;
+  // XCD-aware: hardware places workgroup i on XCD i % 8, so XCD x runs the x-th eighth of the
+  // item-major list (the row blocks of one (pair, direction) share its K / V stream in that L2)
+  const int lw = (G & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3);
+  const int ntiles = a.ntiles;
+  const long long U = (long long)a.nitems * ntiles;
+  long long u = (long long)lw * U / G;
+  const long long u1 = (long long)(lw + 1) * U / G;
+  bool first = true;
+  while (u < u1) {
+    const int item = (int)(u / ntiles), tb = (int)(u % ntiles);
+    const int nt = (int)min((long long)(ntiles - tb), u1 - u);
+    const long long ib = (long long)item * ntiles;
+    const int w0 = q48_owner(ib, U, G), w1 = q48_owner(ib + ntiles - 1, U, G);
+    const bool whole = w0 == w1;
+    if (!first) raw_barrier_r();   // every wave is done with the ring (and the last merge)
+    first = false;
+    q48_segment<MODE>(a, lds, wg_ovf, item, tb, nt, whole ? -1 : item * a.smax + (lw - w0));
+    if (!whole) {
+      // every thread's write-through partial stores acknowledged, then one arrival per segment
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        wg_last = __hip_atomic_fetch_add(a.cnt + item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == w1 - w0;
+      __syncthreads();
+      if (wg_last) {
+        q48_merge<MODE>(a, item, w1 - w0 + 1, item * a.smax);
+        if (threadIdx.x == 0)    // ready for the next launch
+          __hip_atomic_exchange(a.cnt + item, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    u += nt;
+  }
+}
+
+}  // namespace
+
+int coatt_q48_rows() { return RB; }
+
+// Workgroups and partial slots per item for `items` items of `ntiles` key tiles: 256 ranges
+// (one per CU) of >= 8 tile steps each; `cut` false: one workgroup per item, nothing cut.
+static void q48_plan(int items, int ntiles, bool cut, int* nwork, int* smax) {
+  const long long U = (long long)items * ntiles;
+  long long G = cut ? std::min<long long>(256, std::max<long long>(1, U / 8)) : items;
+  if (G <= items) G = items;        // no fewer workgroups than items: at most one cut per item
+  const long long L = U / G;        // shortest range (tile steps)
+  *nwork = (int)G;
+  *smax = (int)((ntiles + L - 1) / L + 1);
+  if (*smax > 8) {                  // the merge holds <= 8 slots: fewer, longer ranges
+    G = std::max<long long>(items, U / ((ntiles + 6) / 7));
+    *nwork = (int)G;
+    *smax = (int)((ntiles + U / G - 1) / (U / G) + 1);
+  }
+}
+
+size_t coatt_q48_workspace_bytes(int items, int ntiles) {
+  int G, smax;
+  q48_plan(items, ntiles, true, &G, &smax);
+  if (G == items) return 0;
+  return (size_t)items * smax * RB * (FD + 2) * sizeof(float) + (size_t)items * sizeof(int) + 16;
+}
+
+int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void* ws,
+                     size_t ws_bytes, hipStream_t st) {
+  a.ndir = nd;
+  a.nrb = (a.HW + RB - 1) / RB;
+  a.nitems = a.nrb * B * nd;
+  a.ntiles = (a.HW + FBK - 1) / FBK;
+  const size_t need = coatt_q48_workspace_bytes(a.nitems, a.ntiles);
+  const bool cut = merge_ok && need && ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0;
+  q48_plan(a.nitems, a.ntiles, cut, &a.nwork, &a.smax);
+  if (a.nwork > a.nitems) {
+    const size_t rows = (size_t)a.nitems * a.smax * RB;
+    a.opart = (float*)ws;
+    a.mlpart = a.opart + rows * FD;
+    a.cnt = (int*)(a.mlpart + rows * 2);
+    const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)a.nitems * sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (mode == 0) hipLaunchKernelGGL(coatt_q48_k<0>, dim3(a.nwork), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(coatt_q48_k<1>, dim3(a.nwork), dim3(256), 0, st, a);
+  CN_CHECK_LAUNCH();
+  return 0;
+}

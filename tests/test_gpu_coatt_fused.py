@@ -251,3 +251,73 @@ def test_split_pair_kernels(cuda, n, hw, var):
         assert (outs[0][k] - v3[k]).abs().max().item() <= 1e-4 * max(1.0, outs[0][k].abs().max().item())
     e = rel(v3[6], outs[0][6].double())
     assert torch.isfinite(v3[6].float()).all() and e <= 8e-3, e
+
+
+def _run_variant(lib, v, vat, va, vb, dzb, n, hw, cuda, acc=0):
+    """No-grad forward, training forward (LSE) and PV backward kernel under variant v."""
+    old = lib.cn_coatt_force_variant(v)
+    assert old != -1
+    try:
+        za, zb = ops.coatt_fused(vat, va, vb, n, hw, torch.empty_like(va), torch.empty_like(va))
+        la = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=cuda)
+        lb = torch.empty_like(la)
+        ta, tb = torch.empty_like(va), torch.empty_like(va)
+        ops.coatt_flash_fwd(vat, va, vb, n, hw, ta, tb, la, lb)
+        pv = (torch.randn((n * hw, 256), generator=torch.Generator().manual_seed(3)) * 0.1) \
+            .to(torch.bfloat16).to(cuda) if acc else torch.zeros_like(va)
+        nws = int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, 1))
+        ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=cuda)
+        nv.call("cn_coatt_flash_pv_ws", vat.data_ptr(), ops.ld(vat), vb.data_ptr(), ops.ld(vb),
+                dzb.data_ptr(), ops.ld(dzb), lb.data_ptr(), n, hw, 256, pv.data_ptr(), ops.ld(pv),
+                acc, ws.data_ptr(), nws, nv.stream())
+        torch.cuda.synchronize()
+    finally:
+        lib.cn_coatt_force_variant(old)
+    return [za, zb, ta, tb, la[:, :hw], lb[:, :hw], pv]
+
+
+@pytest.mark.parametrize("acc", [0, 1])
+@pytest.mark.parametrize("n,hw", [(1, 1), (2, 63), (1, 97), (2, 169), (1, 300), (1, 1271), (4, 3600),
+                                  (5, 3600)])
+def test_q48_kernel(cuda, n, hw, acc):
+    """Variant 5 (coatt_q48_k: 48 query rows per wave, Q in registers, 16x16x32 tiles, a fixed
+    per-row reference maximum) against fp64 of rgbd_segmentation_RAA.py:160-170 (no-grad forward
+    incl. its key-split plan, training forward) and against the 4-wave kernel (variant 1): LSE
+    to 1e-4 (S's summation order differs), the PV backward kernel (plain and accumulating)
+    within the bf16 output rounding."""
+    lib = nv.load()
+    vat, va, vb = make(n, hw, 256, cuda, seed=hw + 13, scale=0.8)
+    g = torch.Generator().manual_seed(n * hw + 2)
+    dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)
+    v1 = _run_variant(lib, 1, vat, va, vb, dzb, n, hw, cuda, acc)
+    v5 = _run_variant(lib, 5, vat, va, vb, dzb, n, hw, cuda, acc)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    for k, (got, ref) in enumerate(((v5[0], ra), (v5[1], rb), (v5[2], ra), (v5[3], rb))):
+        assert torch.isfinite(got.float()).all(), k
+        assert rel(got, ref) <= TOL, (k, rel(got, ref))
+    for k in (4, 5):
+        assert (v1[k] - v5[k]).abs().max().item() <= 1e-4 * max(1.0, v1[k].abs().max().item()), k
+    e = rel(v5[6], v1[6].double())
+    assert torch.isfinite(v5[6].float()).all() and e <= 8e-3, e
+
+
+@pytest.mark.parametrize("n,hw", [(1, 300), (2, 1271), (4, 3600)])
+def test_q48_row_maximum_growth(cuda, n, hw):
+    """The q48 kernel fixes each row's softmax reference at its first key tile's maximum and
+    redoes the workgroup with the exact maxima when a later tile exceeds it by more than 64
+    (log2 units, ~44 in logits).  Keys 200-231 (a later tile) and, in the other direction, query
+    features scaled x8 push the logits' growth far past that: the outputs still match fp64."""
+    lib = nv.load()
+    vat, va, vb = make(n, hw, 256, cuda, seed=hw + 17, scale=0.8)
+    for t in (vb, vat, va):
+        t.view(n, hw, 256)[:, 200:232] *= 8
+    g = torch.Generator().manual_seed(n * hw + 4)
+    dzb = torch.randn((n * hw, 256), generator=g).to(torch.bfloat16).to(cuda)
+    v5 = _run_variant(lib, 5, vat, va, vb, dzb, n, hw, cuda)
+    v1 = _run_variant(lib, 1, vat, va, vb, dzb, n, hw, cuda)
+    ra, rb = ref64(vat, va, vb, n, hw)
+    for k, (got, ref) in enumerate(((v5[0], ra), (v5[1], rb), (v5[2], ra), (v5[3], rb))):
+        assert torch.isfinite(got.float()).all(), k
+        assert rel(got, ref) <= TOL, (k, rel(got, ref))
+    for k in (4, 5):
+        assert (v1[k] - v5[k]).abs().max().item() <= 1e-4 * max(1.0, v1[k].abs().max().item()), k
