@@ -1039,15 +1039,17 @@ static void plan_split(int items, int ntiles, int* nfull, int* nsplit) {
 // Kernel variant: 1 = coatt_fused_fwd_k (4 waves, one per SIMD, 32 rows per wave), 2 =
 // coatt_fused2_k (wave pairs, duplicated S), 3 = coatt_fused3_k (wave pairs splitting the keys),
 // 4 = coatt_dsplit_k (coatt_dsplit.hip: wave pairs splitting the channels, 64 query rows per
-// pair), 5 = coatt_q48_k (coatt_q48.hip: 48 rows per wave, Q in registers, 16x16x32 tiles).
-// CN_COATT_VARIANT picks the default; cn_coatt_force_variant overrides it (tests, A/B tools).
+// pair), 5 = coatt_q48_k (coatt_q48.hip: 48 rows per wave, Q in registers, 16x16x32 tiles,
+// stream-K work split; the default since round 5: 183 vs 224 us at configs[3], 139 vs 165 us for
+// the training forward at 4 pairs, the PV kernel even).  CN_COATT_VARIANT picks the default;
+// cn_coatt_force_variant overrides it (tests, A/B tools).
 static int g_coatt_variant = 0;
 static bool variant_built(int x) { return x == 1 || x == 5 || (CN_EXPERIMENTAL && x >= 2 && x <= 4); }
 static int coatt_variant() {
   static const int v = [] {
     const char* e = getenv("CN_COATT_VARIANT");
-    const int x = e ? atoi(e) : 1;
-    return variant_built(x) ? x : 1;
+    const int x = e ? atoi(e) : 5;
+    return variant_built(x) ? x : 5;
   }();
   return g_coatt_variant ? g_coatt_variant : v;
 }
@@ -1189,6 +1191,27 @@ extern "C" int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void*
   a.accumulate = 0;
   if (coatt_variant() == 5) return q48_launch(0, a, B, nd, false, nullptr, 0, st);
   return fused_launch(0, a, B, nd, st);
+}
+
+extern "C" int cn_coatt_flash_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                     const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                                     void* zb, long long ld_z, float* lse_a, float* lse_b, void* ws,
+                                     size_t ws_bytes, hipStream_t st) {
+  if (coatt_variant() != 5)   // the 4-wave kernel runs the training forward unsplit
+    return cn_coatt_flash_fwd(vat, ld_vat, va, ld_va, vb, ld_vb, B, HW, C, za, zb, ld_z, lse_a, lse_b, st);
+  if (B <= 0 || HW <= 0) return CN_ERR_SHAPE;
+  int rc = fused_check(vat, ld_vat, vb, ld_vb, va, ld_va, ld_z, C);
+  if (rc) return rc;
+  if (((uintptr_t)za & 7) || ((uintptr_t)zb & 7)) return CN_ERR_ALIGN;
+  FusedArgs a = {};
+  int nd = 0;
+  if (za) a.dir[nd++] = FusedDir{(const bf16*)vat, (const bf16*)vb, (const bf16*)vb, (bf16*)za, ld_vat, ld_vb, ld_vb, ld_z, lse_a, nullptr};
+  if (zb) a.dir[nd++] = FusedDir{(const bf16*)vb, (const bf16*)vat, (const bf16*)va, (bf16*)zb, ld_vb, ld_vat, ld_va, ld_z, lse_b, nullptr};
+  if (nd == 0) return CN_ERR_SHAPE;
+  a.HW = HW;
+  a.HWp = (HW + 31) / 32 * 32;
+  const bool merge_ok = !(((uintptr_t)za & 15) || ((uintptr_t)zb & 15) || (ld_z % 8));
+  return q48_launch(0, a, B, nd, merge_ok, ws, ws_bytes, st);
 }
 
 extern "C" int cn_coatt_flash_pv_ws(const void* q, long long ldq, const void* k, long long ldk,

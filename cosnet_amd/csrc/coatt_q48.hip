@@ -50,9 +50,31 @@ namespace {
 constexpr int RW = 48;                 // query rows per wave (3 tiles of 16)
 constexpr int RB = 4 * RW;             // query rows per workgroup (4 waves)
 constexpr int Q48ST = 3;               // K / V ring stages
-constexpr float Q48_GROWTH = 64.0f;    // allowed growth of a row's maximum over its first tile (log2 units)
+// Allowed growth of a row's maximum over its first tile's (log2 units).  P = 2^(s log2e - m) <= 2^96
+// in bf16 (max ~2^128), the fp32 sums <= HW 2^96 |V| -- 2^20 of headroom for |V| x HW / 4096.
+// The training step's own features (tools/probes/q48_step_inputs.py) grow by 42 (median) / 71
+// (p99) / 92 (max) over the first tile: at 64 a quarter of the workgroups redid their keys.
+constexpr float Q48_GROWTH = 96.0f;
 
 __device__ __attribute__((aligned(16))) unsigned g_zero16_q48[4];
+
+// Development timing (make EXTRA_Q48=-DQ48_PROF=1 style builds only): per-phase shader-clock sums
+// of every wave -- [0] DMA wait + barrier, [1] S MFMAs issued, [2] softmax, [3] PV, [4] tiles.
+#ifndef Q48_PROF
+#define Q48_PROF 0
+#endif
+#if Q48_PROF
+__device__ unsigned long long g_q48_prof[8];
+#define Q48_STAMP(k)                                                                          \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory");             \
+    if (k) prof_[(k) - 1] += t_ - prev_;                                                      \
+    prev_ = t_;                                                                               \
+  } while (0)
+#else
+#define Q48_STAMP(k) do {} while (0)
+#endif
 
 __device__ __forceinline__ void glds16r(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -104,6 +126,9 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   const bf16* K = d.k + b * HW * d.ldk;
   const bf16* V = d.v + b * HW * d.ldv;
   const int qw0 = rb * RB + w * RW;          // this wave's first query row
+#if Q48_PROF
+  unsigned long long prof_[5] = {0, 0, 0, 0, 0}, prev_ = 0;
+#endif
   const void* zp = (const void*)g_zero16_q48;
 
   // LDS-DMA: piece i of a tile is, for wave w, K block kb_i = 4 i + w (kt = kb_i >> 3, ds = kb_i & 7)
@@ -117,21 +142,24 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   const unsigned koff = col * ldk2 + g * 16;
   const unsigned voff = vkey * ldv2 + (lane & 1) * 16;
   const int wq = __builtin_amdgcn_readfirstlane(w);
-  const int bp16 = (lane ^ 16) << 2, bp32 = (lane ^ 32) << 2;   // ds_bpermute byte addresses
+  // a uniform 64-bit tile base plus a 32-bit per-lane offset (saddr-form LDS-DMA, no 64-bit
+  // vector adds); the piece's block offset is folded into the per-lane offset
   auto issue_piece = [&](int t, int stage, int i) {
     const int kbi = 4 * i + wq;                    // K block index = V block pair index
     char* kb = lds + stage * 2 * FTILE + kbi * 1024;
     char* vb = lds + stage * 2 * FTILE + FTILE + kbi * 1024;
     const int key0 = (tb + t) * FBK;
-    const char* kr = (const char*)K + (long long)(key0 + 16 * (kbi >> 3)) * ldk2 + (kbi & 7) * 64;
-    const char* vr = (const char*)V + (long long)key0 * ldv2 + kbi * 32;
+    const char* kt = (const char*)K + (size_t)((unsigned)key0 * ldk2);
+    const char* vt = (const char*)V + (size_t)((unsigned)key0 * ldv2);
+    const unsigned ko = koff + (unsigned)(16 * (kbi >> 3)) * ldk2 + (kbi & 7) * 64;
+    const unsigned vo = voff + kbi * 32;
     if (key0 + FBK <= HW) {
-      glds16r(kr + koff, kb);
-      glds16r(vr + voff, vb);
+      glds16r(kt + ko, kb);
+      glds16r(vt + vo, vb);
     } else {   // the last, partial tile: rows past HW read the zero page
       const bool okk = key0 + 16 * (kbi >> 3) + col < HW, okv = key0 + vkey < HW;
-      glds16r(okk ? (const void*)(kr + koff) : zp, kb);
-      glds16r(okv ? (const void*)(vr + voff) : zp, vb);
+      glds16r(okk ? (const void*)(kt + ko) : zp, kb);
+      glds16r(okv ? (const void*)(vt + vo) : zp, vb);
     }
   };
   auto issue = [&](int t, int stage) {
@@ -179,10 +207,13 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   if (nt > 1) issue(1, 1);
 
   int st = 0, st2 = 2;
+  bf16x8 vlast1 = {}, vlast2 = {};   // the last two V fragments handed to MFMAs
   for (int t = 0; t < nt; ++t) {
+    Q48_STAMP(0);
     if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * FTILE / 4096) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier_r();
+    Q48_STAMP(1);
     const bool dodma = t + 2 < nt;
     const int dst2 = st2;
     const char* kb = lds + st * 2 * FTILE;
@@ -207,30 +238,43 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
 #pragma unroll
       for (int qt = 0; qt < 3; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-      // K fragment (A): key 16 kt + col, channels 32 ds + 8 g .. +8 = block 8 kt + ds, slot lane
-      auto kread = [&](int kt, int ds) {
-        return *(const bf16x8*)((const __attribute__((address_space(3))) char*)(uintptr_t)kla + (8 * kt + ds) * 1024);
+      // K fragment (A): key 16 kt + col, channels 32 ds + 8 g .. +8 = block 8 kt + ds, slot lane.
+      // The fragment loads are inline asm with early-clobber outputs that also take the two
+      // fragments consumed last as inputs: an MFMA queued behind its predecessors reads its A / B
+      // registers when it starts, not when it issues, and an LDS load returning into those
+      // registers before that corrupts it (seen as wrong S on the third row tile when the
+      // compiler reloaded a register right behind the MFMA that read it).  Waits are counted here.
+      auto kread = [&](int kt, int ds, const bf16x8& g0, const bf16x8& g1) {
+        bf16x8 r;
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=&v"(r) : "v"(kla), "n"((8 * kt + ds) * 1024), "v"(g0), "v"(g1));
+        return r;
       };
       bf16x8 kf[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) kf[u] = kread(u & 1, u >> 1);
+      for (int u = 0; u < 4; ++u) kf[u] = kread(u & 1, u >> 1, vlast1, vlast2);
+      bf16x8 kprev = vlast1, kprev2 = vlast2;
 #pragma unroll
       for (int it = 0; it < 16; ++it) {          // it = 2 ds + kt
         const int kt = it & 1, ds = it >> 1;
-        const bf16x8 kc = kf[it & 3];
-        if (it + 4 < 16) kf[it & 3] = kread((it + 4) & 1, (it + 4) >> 1);
+        bf16x8 kc = kf[it & 3];
+        if (it + 4 < 16) kf[it & 3] = kread((it + 4) & 1, (it + 4) >> 1, kprev, kprev2);
+        const int younger = 15 - it < 4 ? 15 - it : 4;
+        if (younger == 4) lgkm_wait_r<4>(kc);
+        else if (younger == 3) lgkm_wait_r<3>(kc);
+        else if (younger == 2) lgkm_wait_r<2>(kc);
+        else if (younger == 1) lgkm_wait_r<1>(kc);
+        else lgkm_wait_r<0>(kc);
 #pragma unroll
         for (int qt = 0; qt < 3; ++qt)
           s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kc, qf[qt][ds], s[kt][qt], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-        if (it + 4 < 16) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);   // this step's MFMAs stay ahead of the next loads
+        kprev2 = kprev;
+        kprev = kc;
       }
     }
 
+    Q48_STAMP(2);
     // ---- softmax per row tile: the lane's row q = 16 qt + col, its keys {4g + i, 16 + 4g + i}
     // (pairs of values in packed fp32 FMAs / adds; the partial last tile's key mask as its own
     // copy of the code, not selects on every tile)
@@ -261,8 +305,13 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
         }
         float mx = fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
                          fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
-        mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_ds_bpermute(bp16, __float_as_int(mx))));
-        mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_ds_bpermute(bp32, __float_as_int(mx))));
+        // the row's maximum over the four 16-lane groups: VALU row swaps (no LDS round trips)
+        {
+          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+          mx = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+          mx = fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+        }
         // fixed reference: the row's maximum over its first key tile (O is still zero there, so
         // nothing is rescaled); later tiles may exceed it by up to Q48_GROWTH (log2 units: P and
         // the fp32 sums stay far from overflow), beyond that the row is redone (ovf)
@@ -294,37 +343,52 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
       soft(std::integral_constant<int, 2>{}, std::false_type{});
     }
 
+    Q48_STAMP(3);
     // ---- O^T[16 dt .. +16][q] += V^T P^T: the V^T fragment (A) of channel tile dt in the k order
     // of P: two transposed reads, keys 4g .. 4g+3 and 16 + 4g .. +3; lane 4q4 + p4 of a 16-lane
     // group addresses key row (base + q4), channels 16 dt + 4 p4 .. +3 (8 bytes)
     {
       // block (dt, hi) holds, at lane 16 G + 4 q4 + p4, V[16 hi + 4 G + q4][16 dt + 4 p4 .. +3]
-      auto vread = [&](int dt) {
+      // (loads guarded as the K fragments': never into the registers of the last two fragments)
+      auto vread = [&](int dt, const bf16x8& g0, const bf16x8& g1) {
         u32x2 lo, hi;
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(vla), "n"(dt * 1024));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(vla), "n"(dt * 1024 + 512));
+        asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
+                     : "=&v"(lo), "=&v"(hi)
+                     : "v"(vla), "n"(dt * 1024), "n"(dt * 1024 + 512), "v"(g0), "v"(g1));
         u32x4 v = {lo.x, lo.y, hi.x, hi.y};
         return __builtin_bit_cast(bf16x8, v);
       };
-      constexpr int VPF = 3;
+      constexpr int VPF = 5;
       bf16x8 vf[VPF];
 #pragma unroll
-      for (int u = 0; u < VPF; ++u) vf[u] = vread(u);
+      for (int u = 0; u < VPF; ++u) vf[u] = vread(u, vlast1, vlast2);
+      bf16x8 vprev = vlast1, vprev2 = vlast2;
 #pragma unroll
       for (int dt = 0; dt < 16; ++dt) {
         bf16x8 cur = vf[dt % VPF];
-        if (dt + VPF < 16) vf[dt % VPF] = vread(dt + VPF);
+        if (dt + VPF < 16) vf[dt % VPF] = vread(dt + VPF, vprev, vprev2);
         const int younger = 2 * (15 - dt < VPF ? 15 - dt : VPF);
-        if (younger >= 6) lgkm_wait_r<6>(cur);
+        if (younger >= 10) lgkm_wait_r<10>(cur);
+        else if (younger == 8) lgkm_wait_r<8>(cur);
+        else if (younger == 6) lgkm_wait_r<6>(cur);
         else if (younger == 4) lgkm_wait_r<4>(cur);
         else if (younger == 2) lgkm_wait_r<2>(cur);
         else lgkm_wait_r<0>(cur);
 #pragma unroll
         for (int qt = 0; qt < 3; ++qt)
           o[dt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur, pf[qt], o[dt][qt], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        vprev2 = vprev;
+        vprev = cur;
         if ((dt & 3) == 3 && dodma) issue_piece(t + 2, dst2, dt >> 2);
       }
+      vlast1 = vprev;    // the next tile's K loads stay clear of these
+      vlast2 = vprev2;
     }
+    Q48_STAMP(4);
+#if Q48_PROF
+    prof_[4] += 1;
+#endif
   }
   };
   run(std::integral_constant<int, 0>{});
@@ -334,7 +398,12 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
     const bool wave_ovf = __builtin_amdgcn_ballot_w64(ovf) != 0;   // all lanes vote
     if (lane == 0) wg_ovf[w] = wave_ovf;
     raw_barrier_r();
-    if (wg_ovf[0] | wg_ovf[1] | wg_ovf[2] | wg_ovf[3]) run(std::integral_constant<int, 1>{});
+    if (wg_ovf[0] | wg_ovf[1] | wg_ovf[2] | wg_ovf[3]) {
+#if Q48_PROF
+      if (tid == 0) atomicAdd(&g_q48_prof[5], 1ull);
+#endif
+      run(std::integral_constant<int, 1>{});
+    }
   }
 
   // ---- epilogue: o[dt][qt][i] = O^T[16 dt + 4 g + i][16 qt + col]
@@ -379,6 +448,10 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
       }
     }
   }
+#if Q48_PROF
+  if (lane == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&g_q48_prof[k], prof_[k]);
+#endif
 }
 
 // Merge of a cut item (by its last-arriving segment): slots slot0 .. slot0 + nseg - 1 in order,
@@ -549,3 +622,12 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
   CN_CHECK_LAUNCH();
   return 0;
 }
+
+#if Q48_PROF
+extern "C" int cn_q48_prof_read(unsigned long long* out) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_q48_prof), sizeof(unsigned long long) * 6);
+  if (e != hipSuccess) return (int)e;
+  unsigned long long z[8] = {};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_q48_prof), z, sizeof(z));
+}
+#endif

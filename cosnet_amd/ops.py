@@ -549,9 +549,11 @@ def coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b):
     c = vat.shape[1]
     ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_flash_fwd", n, hw, c),
                      (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
-    nv.call("cn_coatt_flash_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
+    nws = int(nv.query("cn_coatt_fused_workspace_bytes", n, hw, 2))
+    ws = torch.empty((nws // 4,), dtype=torch.float32, device=vat.device) if nws else None
+    nv.call("cn_coatt_flash_fwd_ws", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
             ld(vb), n, hw, c, za.data_ptr(), zb.data_ptr(), ld(za), lse_a.data_ptr(),
-            lse_b.data_ptr(), nv.stream())
+            lse_b.data_ptr(), nv.ptr(ws), nws, nv.stream())
     _prof_end(ev)
 
 

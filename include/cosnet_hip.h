@@ -272,6 +272,13 @@ int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, lon
 int cn_coatt_flash_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
                        const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                        long long ld_z, float* lse_a, float* lse_b, hipStream_t stream);
+/* cn_coatt_flash_fwd with a workspace of cn_coatt_fused_workspace_bytes(B, HW, 2) bytes: with the
+ * 48-row kernel (variant 5) the map's key tiles are then cut across the CUs (stream-K, merged in
+ * the launch); the 4-wave kernel ignores it.  Same results contract as cn_coatt_flash_fwd. */
+int cn_coatt_flash_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                          const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                          long long ld_z, float* lse_a, float* lse_b, void* ws, size_t ws_bytes,
+                          hipStream_t st);
 /* o[q] (+)= sum_k exp2(q.k log2(e) - klse[k]) v[k]: a softmax product whose normaliser is per
  * KEY (the other direction's lse) -- the co-attention backward's dV_a = S_row dZ_b
  * (autograd of rgbd_segmentation_RAA.py:169) with q = Va_t, k = Vb, v = dZ_b, klse = lse_b.
@@ -406,11 +413,12 @@ int cn_gemm_force_config(int cfg);
 /* Development hook (tuning tools only): number of blocks the wgrad K split aims for. */
 int cn_gemm_set_wgrad_target(int blocks);
 /* Development / test hook: co-attention flash forward and PV kernel variant (1: four waves, one
- * per SIMD; 2: eight waves in pairs that split the output channels, S computed by both; 3: pairs
- * that split the keys of S and the output channels; 4: four waves in pairs of 64 query rows that
- * split the channels of S (partial S exchanged through LDS) and of the output; 0: default).
- * Returns the previous setting, or -1 for variants 2-4 in a library built without them
- * (cn_build_experimental() == 0).  CN_COATT_VARIANT sets the default. */
+ * per SIMD, 32 query rows each; 2: eight waves in pairs that split the output channels, S computed
+ * by both; 3: pairs that split the keys of S and the output channels; 4: four waves in pairs of 64
+ * query rows that split the channels of S (partial S exchanged through LDS) and of the output;
+ * 5: four waves of 48 query rows with Q in registers and a stream-K split of the key tiles over
+ * the CUs -- the default; 0: default).  Returns the previous setting, or -1 for variants 2-4 in a
+ * library built without them (cn_build_experimental() == 0).  CN_COATT_VARIANT sets the default. */
 int cn_coatt_force_variant(int v);
 
 #ifdef __cplusplus

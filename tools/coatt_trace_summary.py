@@ -12,7 +12,11 @@ import csv
 import json
 import sys
 
-TRAIN = ("coatt_fused_fwd_k", "coatt_flash_dvat_k", "dvat_sum_k", "coatt_merge_k")
+TRAIN = ("coatt_fused_fwd_k", "coatt_q48_k", "coatt_flash_dvat_k", "dvat_sum_k", "coatt_merge_k")
+# the forward / PV kernel (variant 5 since round 5, variant 1 before) and its split merge
+FWD0 = ("coatt_fused_fwd_k<0>", "coatt_merge_k<0>", "coatt_q48_k<0>")
+PV = ("coatt_fused_fwd_k<1>", "coatt_merge_k<1>", "coatt_q48_k<1>", "dvat_sum_k")
+MAIN0 = ("coatt_fused_fwd_k<0>", "coatt_q48_k<0>")
 
 
 def summarise(path):
@@ -28,17 +32,17 @@ def summarise(path):
     train = [r for r in rows if any(k in name(r) for k in TRAIN) and int(r["Start_Timestamp"]) <= t_last + 1]
     # the PV launch and its merge follow the last dVa_t of the step
     tail = [r for r in rows if int(r["Start_Timestamp"]) > t_last and
-            ("coatt_fused_fwd_k<1>" in name(r) or "coatt_merge_k<1>" in name(r) or "dvat_sum_k" in name(r))]
+            any(k in name(r) for k in PV)]
     train += tail
     c3 = [r for r in rows if int(r["Start_Timestamp"]) > t_last and
-          ("coatt_fused_fwd_k<0>" in name(r) or "coatt_merge_k<0>" in name(r))]
+          any(k in name(r) for k in FWD0)]
     fam = {}
     for r in train:
         k = name(r).replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         f = fam.setdefault(k, [0, 0.0])
         f[0] += 1
         f[1] += dur(r)
-    c3_main = [r for r in c3 if "coatt_fused_fwd_k<0>" in name(r)]
+    c3_main = [r for r in c3 if any(k in name(r) for k in MAIN0)]
     return {"source": path, "steps": steps,
             "train_us_per_step": sum(dur(r) for r in train) / steps,
             "train_families": {k: {"launches_per_step": v[0] / steps, "us_per_step": v[1] / steps}
