@@ -581,16 +581,17 @@ int coatt_q48_rows() { return RB; }
 // (one per CU) of >= 8 tile steps each; `cut` false: one workgroup per item, nothing cut.
 static void q48_plan(int items, int ntiles, bool cut, int* nwork, int* smax) {
   const long long U = (long long)items * ntiles;
-  long long G = cut ? std::min<long long>(256, std::max<long long>(1, U / 8)) : items;
-  if (G <= items) G = items;        // no fewer workgroups than items: at most one cut per item
+  long long G = items;              // uncut: one workgroup per item
+  if (cut) {
+    // 256 equal ranges (also when there are more items than CUs: a range then covers one item
+    // and parts of its neighbours -- one round of 1.2 items beats two rounds of one at 8 pairs)
+    G = std::min<long long>(256, std::max<long long>(1, U / 8));
+    if ((ntiles + U / G - 1) / (U / G) + 1 > 8)   // the merge holds <= 8 slots per item
+      G = std::max<long long>(1, U / ((ntiles + 6) / 7));
+  }
   const long long L = U / G;        // shortest range (tile steps)
   *nwork = (int)G;
   *smax = (int)((ntiles + L - 1) / L + 1);
-  if (*smax > 8) {                  // the merge holds <= 8 slots: fewer, longer ranges
-    G = std::max<long long>(items, U / ((ntiles + 6) / 7));
-    *nwork = (int)G;
-    *smax = (int)((ntiles + U / G - 1) / (U / G) + 1);
-  }
 }
 
 size_t coatt_q48_workspace_bytes(int items, int ntiles) {
@@ -609,7 +610,7 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
   const size_t need = coatt_q48_workspace_bytes(a.nitems, a.ntiles);
   const bool cut = merge_ok && need && ws && ws_bytes >= need && ((uintptr_t)ws & 15) == 0;
   q48_plan(a.nitems, a.ntiles, cut, &a.nwork, &a.smax);
-  if (a.nwork > a.nitems) {
+  if (a.nwork != a.nitems) {
     const size_t rows = (size_t)a.nitems * a.smax * RB;
     a.opart = (float*)ws;
     a.mlpart = a.opart + rows * FD;

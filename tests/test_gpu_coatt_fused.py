@@ -278,13 +278,14 @@ def _run_variant(lib, v, vat, va, vb, dzb, n, hw, cuda, acc=0):
 
 @pytest.mark.parametrize("acc", [0, 1])
 @pytest.mark.parametrize("n,hw", [(1, 1), (2, 63), (1, 97), (2, 169), (1, 300), (1, 1271), (4, 3600),
-                                  (5, 3600)])
+                                  (5, 3600), (8, 3600)])
 def test_q48_kernel(cuda, n, hw, acc):
     """Variant 5 (coatt_q48_k: 48 query rows per wave, Q in registers, 16x16x32 tiles, a fixed
     per-row reference maximum) against fp64 of rgbd_segmentation_RAA.py:160-170 (no-grad forward
     incl. its key-split plan, training forward) and against the 4-wave kernel (variant 1): LSE
     to 1e-4 (S's summation order differs), the PV backward kernel (plain and accumulating)
-    within the bf16 output rounding."""
+    within the bf16 output rounding.  8 pairs: more 192-row items (304) than CUs, each of the
+    256 ranges then spans parts of two items."""
     lib = nv.load()
     vat, va, vb = make(n, hw, 256, cuda, seed=hw + 13, scale=0.8)
     g = torch.Generator().manual_seed(n * hw + 2)

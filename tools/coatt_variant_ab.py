@@ -4,7 +4,7 @@ and the PV backward kernel (4 pairs), 60 x 60 features, C = 256, bf16.  Device t
 a HIP graph of R calls (no host gaps); TFLOP/s counts the executed S and PV products (2 x 2 HW^2 C
 per pair and direction).
 
-    python tools/coatt_variant_ab.py [variants=1,5] [pairs=5,4] [--nograd-only]
+    python tools/coatt_variant_ab.py [variants=1,5] [pairs=5,4] [--nograd-only]   (or 1+5 / 8+4)
 """
 import json
 import os
@@ -46,8 +46,9 @@ def timed(fn):
 def main():
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     nograd_only = "--nograd-only" in sys.argv
-    variants = [int(x) for x in (args[0] if args else "1,5").split(",")]
-    pairs = [int(x) for x in (args[1] if len(args) > 1 else "5,4").split(",")]
+    # lists comma- or plus-separated (tools/gpu_pass.sh py: steps turn commas into spaces)
+    variants = [int(x) for x in (args[0] if args else "1,5").replace("+", ",").split(",")]
+    pairs = [int(x) for x in (args[1] if len(args) > 1 else "5,4").replace("+", ",").split(",")]
     lib = nv.load()
     dev = torch.device("cuda:0")
     hw, c = 3600, 256
@@ -71,7 +72,7 @@ def main():
                 ws = torch.empty((max(nws, 4) // 4,), dtype=torch.float32, device=dev)
                 row = {"variant": v, "n": n,
                        "nograd_fwd_us": timed(lambda: ops.coatt_fused(vat, va, vb, n, hw, za, zb))}
-                if n == 4 and not nograd_only:
+                if n in (4, 8) and not nograd_only:
                     row["train_fwd_us"] = timed(lambda: ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, la, lb))
                     row["pv_us"] = timed(lambda: nv.call(
                         "cn_coatt_flash_pv_ws", vat.data_ptr(), 256, vb.data_ptr(), 256, dzb.data_ptr(), 256,
