@@ -33,12 +33,13 @@
 // co-residency is assumed) merges the item's slots in segment order and writes the output.
 // The merge order is fixed (slots 0, 1, ...), so results do not depend on arrival order.
 // LDS images (one 3-stage ring, 2 x 16 KB per stage) are FRAGMENT-MAJOR: the K image is 16
-// blocks of 1 KB, block (kt, ds) holding at lane slot L the 16 bytes lane L feeds the MFMA
+// blocks of 1 KB, block 2 ds + kt holding at lane slot L the 16 bytes lane L feeds the MFMA
 // (key 16 kt + (L & 15), channels 32 ds + 8 (L >> 4) ..); the V image is 32 blocks of 512 B,
-// block (dt, hi) holding at 8-byte slot L what lane L addresses in its transposed read.  Every
-// fragment read is then one contiguous, conflict-free block at (lane base + immediate offset):
-// no swizzle arithmetic in the loop.  The LDS-DMA fills them with 16-byte chunks gathered from
-// 16 (K) or 32 (V) key rows per 1-KB piece.
+// block (dt, hi) at (dt >> 1) 2048 + (dt & 1) 512 + hi 1024 holding at 8-byte slot L what lane L
+// addresses in its transposed read.  Every fragment read is then one contiguous block at (lane
+// base + immediate offset): no swizzle arithmetic in the loop.  The LDS-DMA fills them with
+// 16-byte chunks gathered from 16 key rows per 1-KB piece.  Where K = V (the Z_a direction: both
+// Vb) the V^T reads address the K image at the same immediates and no V image is loaded.
 #include "common.h"
 #include "coatt_fused.h"
 #include <algorithm>
@@ -131,33 +132,47 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
 #endif
   const void* zp = (const void*)g_zero16_q48;
 
-  // LDS-DMA: piece i of a tile is, for wave w, K block kb_i = 4 i + w (kt = kb_i >> 3, ds = kb_i & 7)
-  // and V block pair dt = 4 i + w.  A lane's global offset is a tile-invariant per-lane part plus
-  // a uniform part: no per-piece vector address arithmetic.
-  //   K block (kt, ds), lane L = (col = L & 15, g = L >> 4): K[key0 + 16 kt + col][32 ds + 8 g .. +8]
-  //   V pair dt, lane L = (hi = L >> 5, g' = (L >> 3) & 3, q4 = (L >> 1) & 3, jl = L & 1):
-  //     V[key0 + 16 hi + 4 g' + q4][16 dt + 8 jl .. +8]
+  // LDS-DMA: piece i of a tile is, for wave w, block index kbi = 4 i + w of both images.
+  // Both images have one layout: block kbi = 2 m + h (m = channel block of 32, h = key half of 16)
+  // holds at 16-byte lane slot L = (c = (L >> 1) & 15, j = 2 (L >> 5) + (L & 1))
+  //   X[key0 + 16 h + c][32 m + 8 j .. +8]        (X = K or V)
+  // so K's S-fragment (kt, ds) is block 2 ds + kt and V's transposed-read block (dt, hi) is at
+  // (dt >> 1) 2048 + (dt & 1) 512 + hi 1024 -- read at lane * 8 from either image (K = V: the
+  // K image, below).
+  // A lane's global offset is a tile-invariant per-lane part plus a uniform part.
   const unsigned ldk2 = (unsigned)d.ldk * 2, ldv2 = (unsigned)d.ldv * 2;
-  const int vkey = 16 * (lane >> 5) + 4 * ((lane >> 3) & 3) + ((lane >> 1) & 3);
-  const unsigned koff = col * ldk2 + g * 16;
-  const unsigned voff = vkey * ldv2 + (lane & 1) * 16;
+  const int vkey = (lane >> 1) & 15;   // + 16 h
+  // The K image has the V image's layout: slot L holds key (L >> 1) & 15, channel group
+  // 2 (L >> 5) + (L & 1).  The S reads (lane = key col, group g) then take slot
+  // 32 (g >> 1) + 2 col + (g & 1) -- conflict-free in the ds_read_b128 lane groups
+  // {0-3,12-15,20-27} / {4-11,16-19,28-31} -- and, when K = V, the V^T reads are the V image's
+  // own lane * 8 pattern on the K image
+  const int kcol = (lane >> 1) & 15;
+  const unsigned koff = kcol * ldk2 + (2 * (lane >> 5) + (lane & 1)) * 16;
+  const unsigned voff = vkey * ldv2 + (2 * (lane >> 5) + (lane & 1)) * 16;
   const int wq = __builtin_amdgcn_readfirstlane(w);
+  // Z_a's direction has K = V = Vb: its V^T fragments are read from the K image and no V image is
+  // loaded -- half the global / L2 traffic of those tiles' LDS-DMA
+  const bool kvs = d.v == d.k && d.ldv == d.ldk;
+  const unsigned voffs = kvs ? 0u : voff;
   // a uniform 64-bit tile base plus a 32-bit per-lane offset (saddr-form LDS-DMA, no 64-bit
   // vector adds); the piece's block offset is folded into the per-lane offset
   auto issue_piece = [&](int t, int stage, int i) {
-    const int kbi = 4 * i + wq;                    // K block index = V block pair index
+    const int kbi = 4 * i + wq;
     char* kb = lds + stage * 2 * FTILE + kbi * 1024;
     char* vb = lds + stage * 2 * FTILE + FTILE + kbi * 1024;
     const int key0 = (tb + t) * FBK;
     const char* kt = (const char*)K + (size_t)((unsigned)key0 * ldk2);
-    const char* vt = (const char*)V + (size_t)((unsigned)key0 * ldv2);
-    const unsigned ko = koff + (unsigned)(16 * (kbi >> 3)) * ldk2 + (kbi & 7) * 64;
-    const unsigned vo = voff + kbi * 32;
+    // K = V: the V piece reads the 16-byte zero page instead (one line; branch-free, so the DMA
+    // issue stays interleaved with the PV MFMAs and the waits keep one count)
+    const char* vt = kvs ? (const char*)zp : (const char*)V + (size_t)((unsigned)key0 * ldv2);
+    const unsigned ko = koff + (unsigned)(16 * (kbi & 1)) * ldk2 + (kbi >> 1) * 64;
+    const unsigned vo = voffs + (kvs ? 0u : (unsigned)(16 * (kbi & 1)) * ldv2 + (kbi >> 1) * 64);
     if (key0 + FBK <= HW) {
       glds16r(kt + ko, kb);
       glds16r(vt + vo, vb);
     } else {   // the last, partial tile: rows past HW read the zero page
-      const bool okk = key0 + 16 * (kbi >> 3) + col < HW, okv = key0 + vkey < HW;
+      const bool okk = key0 + 16 * (kbi & 1) + kcol < HW, okv = key0 + 16 * (kbi & 1) + vkey < HW;
       glds16r(okk ? (const void*)(kt + ko) : zp, kb);
       glds16r(okv ? (const void*)(vt + vo) : zp, vb);
     }
@@ -210,8 +225,11 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   bf16x8 vlast1 = {}, vlast2 = {};   // the last two V fragments handed to MFMAs
   for (int t = 0; t < nt; ++t) {
     Q48_STAMP(0);
-    if (t + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * FTILE / 4096) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t + 1 < nt) {   // tile t landed, tile t+1 (4 or 8 pieces per thread) may be in flight
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * FTILE / 4096) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     raw_barrier_r();
     Q48_STAMP(1);
     const bool dodma = t + 2 < nt;
@@ -222,7 +240,9 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
     const char* vb = kb + FTILE;
     const int key0 = (tb + t) * FBK;
     // the fragment-major images: every fragment read is this lane's slot of one contiguous block
-    const unsigned kla = lds_addr_r(kb) + lane * 16, vla = lds_addr_r(vb) + lane * 8;
+    // V^T read base: lane * 8 in the V image, or (K = V) in the K image, which is laid out alike
+    const unsigned kla = lds_addr_r(kb) + (32 * (g >> 1) + 2 * col + (g & 1)) * 16;
+    const unsigned vla = lds_addr_r(kvs ? kb : vb) + lane * 8;
 
     // MODE 1: the per-key normalisers of the lane's 8 keys {4g + i, 16 + 4g + i}
     f32x4 nk[2];
@@ -238,7 +258,7 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
 #pragma unroll
       for (int qt = 0; qt < 3; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-      // K fragment (A): key 16 kt + col, channels 32 ds + 8 g .. +8 = block 8 kt + ds, slot lane.
+      // K fragment (A): key 16 kt + col, channels 32 ds + 8 g .. +8 = block 2 ds + kt, swizzled slot.
       // The fragment loads are inline asm with early-clobber outputs that also take the two
       // fragments consumed last as inputs: an MFMA queued behind its predecessors reads its A / B
       // registers when it starts, not when it issues, and an LDS load returning into those
@@ -247,7 +267,7 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
       auto kread = [&](int kt, int ds, const bf16x8& g0, const bf16x8& g1) {
         bf16x8 r;
         asm volatile("ds_read_b128 %0, %1 offset:%2"
-                     : "=&v"(r) : "v"(kla), "n"((8 * kt + ds) * 1024), "v"(g0), "v"(g1));
+                     : "=&v"(r) : "v"(kla), "n"((2 * ds + kt) * 1024), "v"(g0), "v"(g1));
         return r;
       };
       bf16x8 kf[4];
@@ -354,7 +374,8 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
         u32x2 lo, hi;
         asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%3\n\tds_read_b64_tr_b16 %1, %2 offset:%4"
                      : "=&v"(lo), "=&v"(hi)
-                     : "v"(vla), "n"(dt * 1024), "n"(dt * 1024 + 512), "v"(g0), "v"(g1));
+                     : "v"(vla), "n"((dt >> 1) * 2048 + (dt & 1) * 512),
+                       "n"((dt >> 1) * 2048 + (dt & 1) * 512 + 1024), "v"(g0), "v"(g1));
         u32x4 v = {lo.x, lo.y, hi.x, hi.y};
         return __builtin_bit_cast(bf16x8, v);
       };
