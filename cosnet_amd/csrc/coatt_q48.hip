@@ -57,8 +57,6 @@ constexpr int Q48ST = 3;               // K / V ring stages
 // (p99) / 92 (max) over the first tile: at 64 a quarter of the workgroups redid their keys.
 constexpr float Q48_GROWTH = 96.0f;
 
-__device__ __attribute__((aligned(16))) unsigned g_zero16_q48[4];
-
 // Development timing (make EXTRA_Q48=-DQ48_PROF=1 style builds only): per-phase shader-clock sums
 // of every wave -- [0] DMA wait + barrier, [1] S MFMAs issued, [2] softmax, [3] PV, [4] tiles.
 #ifndef Q48_PROF
@@ -77,9 +75,9 @@ __device__ unsigned long long g_q48_prof[8];
 #define Q48_STAMP(k) do {} while (0)
 #endif
 
-__device__ __forceinline__ void glds16r(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+__device__ __forceinline__ void blds16q(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base,
+                                           16, (int)voff, 0, 0, 0);
 }
 
 __device__ __forceinline__ void raw_barrier_r() {
@@ -130,7 +128,6 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
 #if Q48_PROF
   unsigned long long prof_[5] = {0, 0, 0, 0, 0}, prev_ = 0;
 #endif
-  const void* zp = (const void*)g_zero16_q48;
 
   // LDS-DMA: piece i of a tile is, for wave w, block index kbi = 4 i + w of both images.
   // Both images have one layout: block kbi = 2 m + h (m = channel block of 32, h = key half of 16)
@@ -154,28 +151,29 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   // Z_a's direction has K = V = Vb: its V^T fragments are read from the K image and no V image is
   // loaded -- half the global / L2 traffic of those tiles' LDS-DMA
   const bool kvs = d.v == d.k && d.ldv == d.ldk;
-  const unsigned voffs = kvs ? 0u : voff;
-  // a uniform 64-bit tile base plus a 32-bit per-lane offset (saddr-form LDS-DMA, no 64-bit
-  // vector adds); the piece's block offset is folded into the per-lane offset
+  // one buffer resource per tile (uniform) plus a 32-bit per-lane offset: the buffer form issues
+  // cheaper than global_load_lds with 64-bit lane addresses (PV phase 1620 -> 1452 clocks per
+  // wave-tile); the piece's block offset is folded into the per-lane offset
   auto issue_piece = [&](int t, int stage, int i) {
     const int kbi = 4 * i + wq;
     char* kb = lds + stage * 2 * FTILE + kbi * 1024;
     char* vb = lds + stage * 2 * FTILE + FTILE + kbi * 1024;
     const int key0 = (tb + t) * FBK;
     const char* kt = (const char*)K + (size_t)((unsigned)key0 * ldk2);
-    // K = V: the V piece reads the 16-byte zero page instead (one line; branch-free, so the DMA
-    // issue stays interleaved with the PV MFMAs and the waits keep one count)
-    const char* vt = kvs ? (const char*)zp : (const char*)V + (size_t)((unsigned)key0 * ldv2);
+    // buffer-form LDS-DMA: the tile's rows as one buffer resource (base = the tile's first row,
+    // range = the rows left), a 32-bit per-lane offset -- rows past HW are out of range and land
+    // as zeros (no partial-tile branch); K = V: the V resource is empty (all zeros, no fetch),
+    // so the DMA issue stays branch-free and interleaved with the PV MFMAs
+    const int left = HW - key0;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(kt), 0, left * (int)ldk2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(kvs ? kt : (const char*)V + (size_t)((unsigned)key0 * ldv2)), 0,
+        kvs ? 0 : left * (int)ldv2, 0x00020000);
     const unsigned ko = koff + (unsigned)(16 * (kbi & 1)) * ldk2 + (kbi >> 1) * 64;
-    const unsigned vo = voffs + (kvs ? 0u : (unsigned)(16 * (kbi & 1)) * ldv2 + (kbi >> 1) * 64);
-    if (key0 + FBK <= HW) {
-      glds16r(kt + ko, kb);
-      glds16r(vt + vo, vb);
-    } else {   // the last, partial tile: rows past HW read the zero page
-      const bool okk = key0 + 16 * (kbi & 1) + kcol < HW, okv = key0 + 16 * (kbi & 1) + vkey < HW;
-      glds16r(okk ? (const void*)(kt + ko) : zp, kb);
-      glds16r(okv ? (const void*)(vt + vo) : zp, vb);
-    }
+    const unsigned vo = voff + (unsigned)(16 * (kbi & 1)) * ldv2 + (kbi >> 1) * 64;
+    blds16q(rk, ko, kb);
+    blds16q(rv, vo, vb);
   };
   auto issue = [&](int t, int stage) {
 #pragma unroll
