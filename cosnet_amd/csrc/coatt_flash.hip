@@ -41,6 +41,11 @@ __device__ __forceinline__ void glds16b(const void* src, char* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+__device__ __forceinline__ void blds16b(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base,
+                                           16, (int)voff, 0, 0, 0);
+}
+
 __device__ __forceinline__ void raw_barrier_b() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -132,27 +137,34 @@ void coatt_flash_dvat_k(BwdArgs a) {
   }
   const bf16* KV = a.vb + b * HW * a.ld_vb;
   const bf16* K2 = T1 ? a.dzb + b * HW * a.ld_dzb : nullptr;
-  // per tile: [Vb rows | Vb transposed | dZb rows]
+  // per tile: [Vb rows | Vb transposed | dZb rows], in buffer form: one resource per tile and
+  // image (base = the tile's first row, range = the rows left: rows past HW land as zeros) and a
+  // 32-bit lane offset -- cheaper to issue than global_load_lds with 64-bit lane addresses.
+  // Piece i covers rows 8 i + (tid >> 5); the chunk swizzle row & 15 alternates with i's parity.
   const int ntiles = (HW + BK - 1) / BK;
   const int tb = split * a.tps;   // first key tile of this work item
+  const unsigned ldb2 = (unsigned)a.ld_vb * 2, ld22 = T1 ? (unsigned)a.ld_dzb * 2 : 0u;
+  const int lrow = tid >> 5, lpos = tid & 31;
+  const unsigned ksw[2] = {(unsigned)((lpos ^ lrow) << 4), (unsigned)((lpos ^ (lrow + 8)) << 4)};
+  const unsigned kof[2] = {lrow * ldb2 + ksw[0], lrow * ldb2 + ksw[1]};
+  const unsigned vof = lrow * ldb2 + (unsigned)((lpos ^ ((lrow & 3) << 2)) << 4);
+  const unsigned k2of[2] = {lrow * ld22 + ksw[0], lrow * ld22 + ksw[1]};
   auto issue = [&](int t, int stage) {
     char* kb = lds + QB + stage * STG;
     const int key0 = (tb + t) * BK;
+    const int left = HW - key0;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(KV + (long long)key0 * a.ld_vb), 0, left * (int)ldb2, 0x00020000);
+    __amdgpu_buffer_rsrc_t r2 = rk;
+    if constexpr (T1)
+      r2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(K2 + (long long)key0 * a.ld_dzb), 0,
+                                             left * (int)ld22, 0x00020000);
 #pragma unroll
     for (int i = 0; i < TILE / 4096; ++i) {
-      const int p = i * 256 + tid;
-      const int row = p >> 5, cpos = p & 31;
-      const int key = key0 + row;
-      const bool ok = key < HW;
       const int wb = (i * 256 + (tid & ~63)) * 16;
-      const bf16* ks = KV + (long long)key * a.ld_vb + ((cpos ^ (row & 15)) << 3);
-      const bf16* vs = KV + (long long)key * a.ld_vb + ((cpos ^ ((row & 3) << 2)) << 3);
-      glds16b(ok ? (const void*)ks : zp, kb + wb);
-      glds16b(ok ? (const void*)vs : zp, kb + TILE + wb);
-      if constexpr (T1) {
-        const bf16* k2 = K2 + (long long)key * a.ld_dzb + ((cpos ^ (row & 15)) << 3);
-        glds16b(ok ? (const void*)k2 : zp, kb + 2 * TILE + wb);
-      }
+      blds16b(rk, kof[i & 1] + 8 * i * ldb2, kb + wb);
+      blds16b(rk, vof + 8 * i * ldb2, kb + TILE + wb);
+      if constexpr (T1) blds16b(r2, k2of[i & 1] + 8 * i * ld22, kb + 2 * TILE + wb);
     }
   };
 

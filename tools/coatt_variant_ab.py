@@ -1,6 +1,6 @@
 """A/B of the co-attention kernel variants (cn_coatt_force_variant) at the bench shapes:
 the no-grad forward (configs[3]: 5 pairs; and 4 pairs), the training forward with LSE (4 pairs)
-and the PV backward kernel (4 pairs), 60 x 60 features, C = 256, bf16.  Device time per call from
+the PV and dVa_t backward kernels (4 / 8 pairs), 60 x 60 features, C = 256, bf16.  Device time per call from
 a HIP graph of R calls (no host gaps); TFLOP/s counts the executed S and PV products (2 x 2 HW^2 C
 per pair and direction).
 
@@ -78,6 +78,9 @@ def main():
                         "cn_coatt_flash_pv_ws", vat.data_ptr(), 256, vb.data_ptr(), 256, dzb.data_ptr(), 256,
                         lb.data_ptr(), n, hw, 256, pv.data_ptr(), 256, 0, ws.data_ptr(), nws, nv.stream()))
                     row["pv_tflops"] = flop_dir / row["pv_us"] / 1e6
+                    # the dVa_t backward kernel (both gradient terms, with its two row-dot passes)
+                    row["dvat_us"] = timed(lambda: ops.coatt_flash_bwd(
+                        vat, va, vb, None, za, zb, la, lb, dzb, dzb, n, hw))
                     row["train_fwd_tflops"] = 2 * flop_dir / row["train_fwd_us"] / 1e6
                 row["nograd_fwd_tflops"] = 2 * flop_dir / row["nograd_fwd_us"] / 1e6
             finally:
