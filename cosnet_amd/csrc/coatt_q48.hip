@@ -80,6 +80,14 @@ __device__ __forceinline__ void blds16q(__amdgpu_buffer_rsrc_t r, unsigned voff,
                                            16, (int)voff, 0, 0, 0);
 }
 
+// maximum over the four 16-lane groups holding one row's keys: VALU row swaps (no LDS round trip)
+__device__ __forceinline__ float row_max_r(float x) {
+  const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+  const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+
 __device__ __forceinline__ void raw_barrier_r() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -208,7 +216,7 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   constexpr int pass = decltype(passc)::value;
   if (pass) {
 #pragma unroll
-    for (int qt = 0; qt < 3; ++qt) m[qt] = mt[qt];
+    for (int qt = 0; qt < 3; ++qt) m[qt] = row_max_r(mt[qt]);   // the lanes' maxima, per row
   }
 #pragma unroll
   for (int dt = 0; dt < 16; ++dt)
@@ -321,20 +329,17 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
           for (int j = 0; j < 8; ++j)
             if (key0 + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4) >= HW) v[j >> 1][j & 1] = -INFINITY;
         }
-        float mx = fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
-                         fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
-        // the row's maximum over the four 16-lane groups: VALU row swaps (no LDS round trips)
-        {
-          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-          mx = fmaxf(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
-          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-          mx = fmaxf(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
-        }
+        // this lane's maximum over its 8 keys
+        const float mx = fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
+                               fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
         // fixed reference: the row's maximum over its first key tile (O is still zero there, so
         // nothing is rescaled); later tiles may exceed it by up to Q48_GROWTH (log2 units: P and
-        // the fp32 sums stay far from overflow), beyond that the row is redone (ovf)
+        // the fp32 sums stay far from overflow), beyond that the row is redone (ovf).  Only the
+        // first tile needs the row maximum across the lanes; later tiles check each lane's own
+        // maximum (a row outgrows its reference iff one of its lanes does) and keep per-lane
+        // running maxima, reduced per row only if the redo pass runs
         if constexpr (pass == 0) {
-          if (t == 0) m[qt] = mx * L2E;
+          if (t == 0) m[qt] = row_max_r(mx) * L2E;
           else ovf |= mx * L2E > m[qt] + Q48_GROWTH;
           mt[qt] = fmaxf(mt[qt], mx * L2E);
         }
