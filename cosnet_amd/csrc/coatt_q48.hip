@@ -51,11 +51,12 @@ namespace {
 constexpr int RW = 48;                 // query rows per wave (3 tiles of 16)
 constexpr int RB = 4 * RW;             // query rows per workgroup (4 waves)
 constexpr int Q48ST = 3;               // K / V ring stages
-// Allowed growth of a row's maximum over its first tile's (log2 units).  P = 2^(s log2e - m) <= 2^96
-// in bf16 (max ~2^128), the fp32 sums <= HW 2^96 |V| -- 2^20 of headroom for |V| x HW / 4096.
-// The training step's own features (tools/probes/q48_step_inputs.py) grow by 42 (median) / 71
-// (p99) / 92 (max) over the first tile: at 64 a quarter of the workgroups redid their keys.
-constexpr float Q48_GROWTH = 96.0f;
+// Bound on a lane's partial softmax sum under the first tile's reference: every P it added is
+// <= 2^100 (bf16 max ~2^128) and the fp32 O sums <= HW 2^100 |V| -- 2^15 of headroom for
+// |V| x HW / 4096; an overflow to inf also fails it.  The training step's own features
+// (tools/probes/q48_step_inputs.py) grow by 42 (median) / 71 (p99) / 92 (max) log2 units over the
+// first tile, so no workgroup redoes its keys on them.
+constexpr float Q48_LMAX = 0x1p100f;
 
 // Development timing (make EXTRA_Q48=-DQ48_PROF=1 style builds only): per-phase shader-clock sums
 // of every wave -- [0] DMA wait + barrier, [1] S MFMAs issued, [2] softmax, [3] PV, [4] tiles.
@@ -210,11 +211,12 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   bool ovf = false;
   const float L2E = 1.4426950408889634f;
 
-  // pass 0: reference = each row's maximum over its first tile; pass 1 (only when a row of the
-  // workgroup outgrew its reference by more than Q48_GROWTH): again with the exact maxima
+  // pass 0: reference = each row's maximum over its first tile; only when a lane's partial sum
+  // ends above Q48_LMAX (a logit outgrew the reference; an overflow lands there as inf) does the
+  // workgroup run pass 2 (S only: the exact row maxima) and pass 1 (again, with those maxima)
   auto run = [&](auto passc) {
   constexpr int pass = decltype(passc)::value;
-  if (pass) {
+  if (pass == 1) {
 #pragma unroll
     for (int qt = 0; qt < 3; ++qt) m[qt] = row_max_r(mt[qt]);   // the lanes' maxima, per row
   }
@@ -329,19 +331,19 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
           for (int j = 0; j < 8; ++j)
             if (key0 + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4) >= HW) v[j >> 1][j & 1] = -INFINITY;
         }
-        // this lane's maximum over its 8 keys
-        const float mx = fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
-                               fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
         // fixed reference: the row's maximum over its first key tile (O is still zero there, so
-        // nothing is rescaled); later tiles may exceed it by up to Q48_GROWTH (log2 units: P and
-        // the fp32 sums stay far from overflow), beyond that the row is redone (ovf).  Only the
-        // first tile needs the row maximum across the lanes; later tiles check each lane's own
-        // maximum (a row outgrows its reference iff one of its lanes does) and keep per-lane
-        // running maxima, reduced per row only if the redo pass runs
+        // nothing is rescaled); later tiles are not checked one by one -- the lanes' partial sums
+        // bound every P they added, and a sum above Q48_LMAX at the end makes the workgroup redo
+        // its keys.  Pass 2 only tracks this lane's running maximum.
+        auto lane_max = [&]() {
+          return fmaxf(fmaxf(fmaxf(v[0].x, v[0].y), fmaxf(v[1].x, v[1].y)),
+                       fmaxf(fmaxf(v[2].x, v[2].y), fmaxf(v[3].x, v[3].y)));
+        };
         if constexpr (pass == 0) {
-          if (t == 0) m[qt] = row_max_r(mx) * L2E;
-          else ovf |= mx * L2E > m[qt] + Q48_GROWTH;
-          mt[qt] = fmaxf(mt[qt], mx * L2E);
+          if (t == 0) m[qt] = row_max_r(lane_max()) * L2E;
+        } else if constexpr (pass == 2) {
+          mt[qt] = fmaxf(mt[qt], lane_max() * L2E);
+          return;
         }
         const f32x2 nm = {-m[qt], -m[qt]};
 #pragma unroll
@@ -370,7 +372,12 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
     // ---- O^T[16 dt .. +16][q] += V^T P^T: the V^T fragment (A) of channel tile dt in the k order
     // of P: two transposed reads, keys 4g .. 4g+3 and 16 + 4g .. +3; lane 4q4 + p4 of a 16-lane
     // group addresses key row (base + q4), channels 16 dt + 4 p4 .. +3 (8 bytes)
-    {
+    if constexpr (pass == 2) {   // S only: tile t + 2's DMA pieces, no PV
+      if (dodma) {
+#pragma unroll
+        for (int i = 0; i < FTILE / 4096; ++i) issue_piece(t + 2, dst2, i);
+      }
+    } else {
       // block (dt, hi) holds, at lane 16 G + 4 q4 + p4, V[16 hi + 4 G + q4][16 dt + 4 p4 .. +3]
       // (loads guarded as the K fragments': never into the registers of the last two fragments)
       auto vread = [&](int dt, const bf16x8& g0, const bf16x8& g1) {
@@ -417,8 +424,10 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
   };
   run(std::integral_constant<int, 0>{});
   if constexpr (MODE == 0) {
-    // any overflow in the workgroup?  (the barrier also retires every wave's reads of the ring
-    // before pass 1's DMA refills it)
+    // any lane's partial sum past Q48_LMAX in the workgroup?  (the barrier also retires every
+    // wave's reads of the ring before the redo's DMA refills it)
+#pragma unroll
+    for (int qt = 0; qt < 3; ++qt) ovf |= fmaxf(l[qt].x, l[qt].y) > Q48_LMAX;
     const bool wave_ovf = __builtin_amdgcn_ballot_w64(ovf) != 0;   // all lanes vote
     if (lane == 0) wg_ovf[w] = wave_ovf;
     raw_barrier_r();
@@ -426,6 +435,8 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
 #if Q48_PROF
       if (tid == 0) atomicAdd(&g_q48_prof[5], 1ull);
 #endif
+      run(std::integral_constant<int, 2>{});   // the exact row maxima
+      raw_barrier_r();                          // every wave done with the ring before the refill
       run(std::integral_constant<int, 1>{});
     }
   }

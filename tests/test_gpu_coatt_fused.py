@@ -305,8 +305,9 @@ def test_q48_kernel(cuda, n, hw, acc):
 @pytest.mark.parametrize("n,hw", [(1, 300), (2, 1271), (4, 3600)])
 def test_q48_row_maximum_growth(cuda, n, hw):
     """The q48 kernel fixes each row's softmax reference at its first key tile's maximum and
-    redoes the workgroup with the exact maxima when a later tile exceeds it by more than 96
-    (log2 units, ~67 in logits).  Keys 200-231 (a later tile) and, in the other direction, query
+    redoes the workgroup (an S-only pass for the exact maxima, then again with them) when a lane's
+    partial sum ends above 2^100, i.e. a later logit outgrew the reference by ~100 log2 units (~69
+    in logits) or overflowed.  Keys 200-231 (a later tile) and, in the other direction, query
     features scaled x8 push the logits' growth far past that: the outputs still match fp64."""
     lib = nv.load()
     vat, va, vb = make(n, hw, 256, cuda, seed=hw + 17, scale=0.8)
