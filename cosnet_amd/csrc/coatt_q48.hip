@@ -452,9 +452,17 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
       if (qrow < HW) {
         const unsigned prow = (unsigned)slot * RB + (unsigned)(qrow - rb * RB);
         const __amdgpu_buffer_rsrc_t ro = part_rsrc(a.opart);
+        // partial O in bf16 (half the write-through bytes; the merge folds <= 8 slots in fp32)
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4p;
+        typedef __attribute__((ext_vector_type(2))) float f32x2p;
 #pragma unroll
-        for (int dt = 0; dt < 16; ++dt)
-          __builtin_amdgcn_raw_buffer_store_b128(o[dt][qt], ro, (prow * FD + 4 * g + 16 * dt) * 4, 0, CP_SYS);
+        for (int dt = 0; dt < 16; ++dt) {
+          bf16x4p h;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) h[j] = (bf16)o[dt][qt][j];
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(f32x2p, h), ro,
+                                                (prow * FD + 4 * g + 16 * dt) * 2, 0, CP_SYS);
+        }
         if (MODE == 0 && g == 0) {
           typedef __attribute__((ext_vector_type(2))) float f32x2;
           __builtin_amdgcn_raw_buffer_store_b64(f32x2{m[qt], lt}, part_rsrc(a.mlpart), prow * 8, 0, CP_SYS);
@@ -513,15 +521,14 @@ __device__ __forceinline__ void q48_merge(const FusedArgs& a, int item, int nseg
       for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
     }
     for (int s = 0; s < nseg; ++s) {
-      f32x4 v0[MB], v1[MB];
+      bf16x8 pv[MB];
       f32x2 ml[MB];
 #pragma unroll
       for (int j = 0; j < MB; ++j) {
         const int idx = base + j * 256 + threadIdx.x;
         const unsigned prow = (unsigned)(slot0 + s) * RB + idx / (FD / 8);
-        const unsigned off = (prow * FD + (idx % (FD / 8)) * 8) * 4;
-        v0[j] = __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, CP_SYS);
-        v1[j] = __builtin_amdgcn_raw_buffer_load_b128(ro, off + 16, 0, CP_SYS);
+        const unsigned off = (prow * FD + (idx % (FD / 8)) * 8) * 2;   // bf16 partial rows
+        pv[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, CP_SYS));
         if constexpr (MODE == 0) ml[j] = __builtin_amdgcn_raw_buffer_load_b64(rml, prow * 8, 0, CP_SYS);
       }
 #pragma unroll
@@ -535,10 +542,7 @@ __device__ __forceinline__ void q48_merge(const FusedArgs& a, int item, int nseg
           L[j] = fmaf(ml[j].y, ws, L[j] * wo);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[j][e] = fmaf(v0[j][e], ws, acc[j][e] * wo);
-          acc[j][4 + e] = fmaf(v1[j][e], ws, acc[j][4 + e] * wo);
-        }
+        for (int e = 0; e < 8; ++e) acc[j][e] = fmaf((float)pv[j][e], ws, acc[j][e] * wo);
       }
     }
 #pragma unroll
@@ -582,6 +586,10 @@ void coatt_q48_k(FusedArgs a) {
   long long u = (long long)lw * U / G;
   const long long u1 = (long long)(lw + 1) * U / G;
   bool first = true;
+#if Q48_PROF
+  const unsigned long long k0_ = __builtin_amdgcn_s_memtime();
+  unsigned long long mg_ = 0;
+#endif
   while (u < u1) {
     const int item = (int)(u / ntiles), tb = (int)(u % ntiles);
     const int nt = (int)min((long long)(ntiles - tb), u1 - u);
@@ -599,13 +607,25 @@ void coatt_q48_k(FusedArgs a) {
         wg_last = __hip_atomic_fetch_add(a.cnt + item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == w1 - w0;
       __syncthreads();
       if (wg_last) {
+#if Q48_PROF
+        const unsigned long long m0_ = __builtin_amdgcn_s_memtime();
+#endif
         q48_merge<MODE>(a, item, w1 - w0 + 1, item * a.smax);
+#if Q48_PROF
+        mg_ += __builtin_amdgcn_s_memtime() - m0_;
+#endif
         if (threadIdx.x == 0)    // ready for the next launch
           __hip_atomic_exchange(a.cnt + item, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     u += nt;
   }
+#if Q48_PROF
+  if (threadIdx.x == 0) {   // whole-workgroup clocks and merge clocks
+    atomicAdd(&g_q48_prof[6], __builtin_amdgcn_s_memtime() - k0_);
+    atomicAdd(&g_q48_prof[7], mg_);
+  }
+#endif
 }
 
 }  // namespace
@@ -633,7 +653,8 @@ size_t coatt_q48_workspace_bytes(int items, int ntiles) {
   int G, smax;
   q48_plan(items, ntiles, true, &G, &smax);
   if (G == items) return 0;
-  return (size_t)items * smax * RB * (FD + 2) * sizeof(float) + (size_t)items * sizeof(int) + 16;
+  // bf16 partial O rows, fp32 (reference, sum) pairs, the arrival counters
+  return (size_t)items * smax * RB * (FD * sizeof(bf16) + 2 * sizeof(float)) + (size_t)items * sizeof(int) + 16;
 }
 
 int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void* ws,
@@ -647,8 +668,8 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
   q48_plan(a.nitems, a.ntiles, cut, &a.nwork, &a.smax);
   if (a.nwork != a.nitems) {
     const size_t rows = (size_t)a.nitems * a.smax * RB;
-    a.opart = (float*)ws;
-    a.mlpart = a.opart + rows * FD;
+    a.opart = (float*)ws;                  // bf16 rows of FD channels
+    a.mlpart = a.opart + rows * FD / 2;
     a.cnt = (int*)(a.mlpart + rows * 2);
     const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)a.nitems * sizeof(int), st);
     if (e != hipSuccess) return (int)e;
@@ -661,7 +682,7 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
 
 #if Q48_PROF
 extern "C" int cn_q48_prof_read(unsigned long long* out) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_q48_prof), sizeof(unsigned long long) * 6);
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_q48_prof), sizeof(unsigned long long) * 8);
   if (e != hipSuccess) return (int)e;
   unsigned long long z[8] = {};
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_q48_prof), z, sizeof(z));

@@ -244,7 +244,8 @@ int cn_coatt_fused_fwd(const void* vat, long long ld_vat, const void* va, long l
 /* Same product with the keys split over several workgroups per query block when one
  * workgroup per (row block, pair, direction) would leave most of the last round of CUs idle
  * (configs[3]: 5 pairs -> 290 workgroups on 256 CUs): each split writes its un-normalised
- * fp32 partial O and row (max, sum) into ws, a merge kernel folds them in split order.
+ * partial O (bf16 in the default 48-row kernel, fp32 in the 4-wave one) and fp32 row (max, sum)
+ * into ws, and the partials are folded in split order (in the launch, or by a merge kernel).
  * ws_bytes >= cn_coatt_fused_workspace_bytes(B, HW, ndir) (0: no split, ws may be NULL);
  * za/zb 16-byte aligned, ld_z % 8 == 0.  A NULL / too small / misaligned ws is not an error:
  * the launch then runs unsplit (same result, slower tail). */
@@ -287,8 +288,9 @@ int cn_coatt_flash_pv(const void* q, long long ldq, const void* k, long long ldk
                       long long ldv, const float* klse, int B, int HW, int C, void* o, long long ldo,
                       int accumulate, hipStream_t stream);
 /* Same, with a workspace (>= cn_coatt_fused_workspace_bytes(B, HW, 1)) that lets the keys of
- * an under-filled last round of workgroups be split over several workgroups (fp32 partials
- * summed in split order); without one (NULL / too small) it runs unsplit. */
+ * an under-filled last round of workgroups be split over several workgroups (partials summed
+ * in split order in fp32; bf16 partial rows in the 48-row kernel); without one (NULL / too
+ * small) it runs unsplit. */
 int cn_coatt_flash_pv_ws(const void* q, long long ldq, const void* k, long long ldk, const void* v,
                          long long ldv, const float* klse, int B, int HW, int C, void* o,
                          long long ldo, int accumulate, void* ws, size_t ws_bytes, hipStream_t stream);

@@ -13,7 +13,7 @@ from cosnet_amd import ops             # noqa: E402
 
 dev = torch.device("cuda:0")
 lib = nv.load()
-buf = (ctypes.c_ulonglong * 5)()
+buf = (ctypes.c_ulonglong * 8)()
 for n, hw, mode in ((5, 3600, "nograd"), (4, 3600, "train")):
     g = torch.Generator().manual_seed(n)
     vat, va, vb = [(torch.randn((n * hw, 256), generator=g) * 0.7).to(torch.bfloat16).to(dev) for _ in range(3)]
@@ -40,3 +40,9 @@ for n, hw, mode in ((5, 3600, "nograd"), (4, 3600, "train")):
     print(n, hw, mode, "kernel us %.1f" % (e0.elapsed_time(e1) / 10 * 1e3), "wave-tiles", tiles // 10,
           "cycles/wave-tile %.0f" % tot,
           " ".join("%s %.0f (%.0f%%)" % (nm, x / tiles, 100 * x / tiles / tot) for nm, x in zip(names, v[:4])))
+    # whole-workgroup clocks vs the tile loop's (per wave: the 4 phases summed over a WG's 4 waves)
+    nwg = int(nv.query("cn_coatt_q48_nwork", n, hw)) if hasattr(lib, "cn_coatt_q48_nwork") else 256
+    wg = v[6] / 10 / nwg
+    loop = sum(v[:4]) / 10 / nwg / 4
+    print("   per workgroup: kernel clocks %.0f, tile loop %.0f (%.0f%%), merges %.0f (%.0f%%), rest %.0f" %
+          (wg, loop, 100 * loop / wg, v[7] / 10 / nwg, 100 * v[7] / 10 / nwg / wg, wg - loop - v[7] / 10 / nwg))
