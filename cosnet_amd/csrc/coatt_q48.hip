@@ -452,16 +452,19 @@ __device__ __forceinline__ void q48_segment(const FusedArgs& a, char* lds, int* 
       if (qrow < HW) {
         const unsigned prow = (unsigned)slot * RB + (unsigned)(qrow - rb * RB);
         const __amdgpu_buffer_rsrc_t ro = part_rsrc(a.opart);
-        // partial O in bf16 (half the write-through bytes; the merge folds <= 8 slots in fp32)
-        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4p;
-        typedef __attribute__((ext_vector_type(2))) float f32x2p;
+        // partial O in bf16 (half the write-through bytes; the merge folds <= 8 slots in fp32),
+        // 16-byte chunk 4 p + g of the row = channels 32 p + 4 g .. +3 and 32 p + 16 + 4 g .. +3
+        // (one dwordx4 store per channel-tile pair)
 #pragma unroll
-        for (int dt = 0; dt < 16; ++dt) {
-          bf16x4p h;
+        for (int pp = 0; pp < 8; ++pp) {
+          bf16x8 h;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) h[j] = (bf16)o[dt][qt][j];
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(f32x2p, h), ro,
-                                                (prow * FD + 4 * g + 16 * dt) * 2, 0, CP_SYS);
+          for (int j = 0; j < 4; ++j) {
+            h[j] = (bf16)o[2 * pp][qt][j];
+            h[4 + j] = (bf16)o[2 * pp + 1][qt][j];
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, h), ro,
+                                                 (prow * FD + 8 * (4 * pp + g)) * 2, 0, CP_SYS);
         }
         if (MODE == 0 && g == 0) {
           typedef __attribute__((ext_vector_type(2))) float f32x2;
@@ -548,25 +551,35 @@ __device__ __forceinline__ void q48_merge(const FusedArgs& a, int item, int nseg
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       const int idx = base + j * 256 + threadIdx.x;
-      const int row = idx / (FD / 8), c0 = (idx % (FD / 8)) * 8;
+      const int row = idx / (FD / 8), k = idx % (FD / 8);
+      // chunk k = 4 p + g of a partial row: channels 32 p + 4 g .. +3 and 32 p + 16 + 4 g .. +3
+      const int c0 = 32 * (k >> 2) + 4 * (k & 3);
       const int q = rb * RB + row;
       if (q >= a.HW) {
-        if (MODE == 0 && d.lse && c0 == 0 && q < a.HWp) d.lse[b * a.HWp + q] = INFINITY;
+        if (MODE == 0 && d.lse && k == 0 && q < a.HWp) d.lse[b * a.HWp + q] = INFINITY;
         continue;
       }
       bf16* op = d.o + (b * a.HW + q) * d.ldo + c0;
       const float inv = MODE == 0 ? 1.f / L[j] : 1.f;
-      bf16x8 outv;
+      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4m;
+      bf16x4m lo, hi;
       if (MODE == 1 && a.accumulate) {
-        const bf16x8 old = *(const bf16x8*)op;
+        const bf16x4m olo = *(const bf16x4m*)op, ohi = *(const bf16x4m*)(op + 16);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) outv[e] = (bf16)(acc[j][e] + (float)old[e]);
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = (bf16)(acc[j][e] + (float)olo[e]);
+          hi[e] = (bf16)(acc[j][4 + e] + (float)ohi[e]);
+        }
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) outv[e] = (bf16)(acc[j][e] * inv);
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = (bf16)(acc[j][e] * inv);
+          hi[e] = (bf16)(acc[j][4 + e] * inv);
+        }
       }
-      *(bf16x8*)op = outv;
-      if (MODE == 0 && d.lse && c0 == 0) d.lse[b * a.HWp + q] = M[j] + __builtin_amdgcn_logf(L[j]);
+      *(bf16x4m*)op = lo;
+      *(bf16x4m*)(op + 16) = hi;
+      if (MODE == 0 && d.lse && k == 0) d.lse[b * a.HWp + q] = M[j] + __builtin_amdgcn_logf(L[j]);
     }
   }
 }
