@@ -110,8 +110,11 @@ def parse():
                          "timed on one GPU (the line says parallelism dp1-chain)")
     ap.add_argument("--grad-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="data-parallel gradient buckets reduced in fp32 (default) or bf16")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse the multi-rank path on one device (not a measurement)")
+    ap.add_argument("--dist-backend", default=None, choices=["nccl", "gloo"],
+                    help="N > 1: nccl (RCCL, the default) or gloo (rehearse the multi-rank path on "
+                         "one device, not a measurement).  N = 1 with --dp-chain 1 and nccl: a "
+                         "world-1 RCCL process group with the chain's all-reduces really issued "
+                         "(parallelism dp1-chain-rccl)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group plumbing only (no model, no GPU)")
     return ap.parse_args()
@@ -337,15 +340,36 @@ def dry_run(args, world, rank):
         print(json.dumps({"metric": "dry-run (launcher plumbing only)", "value": None,
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "max_rank_seconds": dt,
-                          "config": {"parallelism": "dp%d" % world}}), flush=True)
+                          "config": {"parallelism": "dp%d" % world}}), file=_json_out(), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+_JSON_OUT = None
+
+
+def _json_out():
+    return _JSON_OUT or sys.stdout
+
+
+def _claim_stdout():
+    """The JSON line is the only thing this process writes to stdout: native libraries print to
+    fd 1 too (RCCL's version banner at communicator init), so fd 1 becomes a copy of stderr and
+    the line goes to a private duplicate of the original stdout."""
+    global _JSON_OUT
+    try:
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+    except OSError:
+        _JSON_OUT = None
 
 
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return _launch_ranks(args.gpus, sys.argv[1:])
+    _claim_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and "WORLD_SIZE" in os.environ:
         print("[bench] note: --gpus %d but WORLD_SIZE=%d; the launcher's world size is used"
@@ -358,15 +382,21 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist_backend == "gloo":   # rehearsal: every rank on device 0
+    backend = args.dist_backend or "nccl"
+    if backend == "gloo":   # rehearsal: every rank on device 0
         local = 0
-    if world > 1:
+    # world-1 RCCL chain: configs[2]'s per-rank step with its collectives issued on a real
+    # RCCL communicator (one rank, this device)
+    rccl1 = world == 1 and args.dp_chain and args.dist_backend == "nccl"
+    if world > 1 or rccl1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init = {} if world > 1 else {"init_method": "tcp://127.0.0.1:%d" % _free_port(),
+                                     "world_size": 1, "rank": 0}
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), **init)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **init)
     dev = torch.device("cuda", local)
 
     import cosnet_amd as C
@@ -390,7 +420,7 @@ def main():
 
     B, S = args.batch, args.size
     step = TrainStep(model, opt, B, S, graphed=bool(args.graph), grad_dtype=args.grad_dtype,
-                     dp_chain=bool(args.dp_chain))
+                     dp_chain=bool(args.dp_chain), collectives=bool(rccl1))
     step.load(*[t.to(dev) for t in synthetic_inputs(B, S, S, seed=1234 + rank)])
     max_iter = 10000
 
@@ -460,9 +490,10 @@ def main():
                                "batch %d pairs/GPU" % (S, S, B),
                    "model": "RGBDSegmentation_RAA(Bottleneck,[3,4,23,3],[3,4,6,3],1)",
                    "global_batch": B * world, "image_hw": [S, S],
-                   "parallelism": "dp%d" % world + ("-chain" if args.dp_chain and world == 1 else ""),
+                   "parallelism": "dp%d" % world + ("-chain" if args.dp_chain and world == 1 else "")
+                                  + ("-rccl" if rccl1 else ""),
                    "grad_reduce": "%s buckets overlapped with the encoder backward" % args.grad_dtype
-                   if world > 1 else None,
+                   if world > 1 or rccl1 else None,
                    "loss": float(loss.item())},
         "model_tflops_per_s": pairs * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None,
     }
@@ -563,8 +594,8 @@ def main():
         except Exception as e:  # report, never hide
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=_json_out(), flush=True)
+    if world > 1 or rccl1:
         dist.destroy_process_group()
 
 

@@ -67,6 +67,27 @@ WGRAD_FP8 = os.environ.get("CN_WGRAD_FP8", "1") != "0"
 _PROBE_SKIP = int(os.environ.get("CN_PROBE_SKIP_APPLY", "0"))
 
 
+# The per-module path (functions.StemFn / BottleneckFn / ASPPFn: frames of different sizes, e.g.
+# configs[3]'s 1 target vs 5 references) runs the block functions below with one segment and
+# without fp8 (its calls bracket no Fp8Acts pass): _FP8_OFF[0] is set around them.
+_FP8_OFF = [False]
+
+
+def fp8_of(mod):
+    """The fp8 context a module's convs use (None: bf16 / fp32 operands)."""
+    return None if _FP8_OFF[0] else getattr(mod, "_cn_fp8", None)
+
+
+class no_fp8:
+    def __enter__(self):
+        self.prev = _FP8_OFF[0]
+        _FP8_OFF[0] = True
+
+    def __exit__(self, *a):
+        _FP8_OFF[0] = self.prev
+        return False
+
+
 def _layer_index(enc):
     """id(block) -> index of its ResNet layer."""
     bb = enc.backbone
@@ -171,7 +192,7 @@ def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=
     list q8 the e4m3 input copy is appended to it as Fp8Acts.saved() (for the fp8 weight
     gradient)."""
     cin = wf.shape[1] // (k * k)
-    ctx = getattr(bn, "_cn_fp8", None)
+    ctx = fp8_of(bn)
     if weight is not None and ctx is not None and fp8_ok(x, cin) and x.shape[0] > 64:
         x8, xs = ctx.acts.quant(x, id(weight))
         if q8 is not None:
@@ -192,7 +213,7 @@ def seg_apply(x, stats, bn, act=0, prelu=None, res=None, xr=None, rstats=None, r
     output in the same pass (delayed scaling; a first use calibrates by a separate pass); with
     mask (ops.relu_mask) also the ReLU mask bits the backward reads instead of the output."""
     rs = None if rstats is None else (rstats.mean, rstats.invstd)
-    ctx = getattr(bn, "_cn_fp8", None)
+    ctx = fp8_of(bn)
     if fp8_key is None or ctx is None or x.dtype != torch.bfloat16:
         return bn_apply(x, (stats.mean, stats.invstd), bn, act=act, prelu=prelu, res=res, xr=xr,
                         rstats=rs, rbn=rbn, out=out, nseg=stats.nseg, mask=mask)
@@ -362,7 +383,7 @@ def bottleneck_bwd(item, dy, grads, need_dx=True, wq=None):
                 dw=grads.buf(blk.conv3.weight, 4 * planes, planes))
     # dgrads, fused with the reduction of the backward of the BN + ReLU that fed the conv where
     # that is cheaper (fuse_bwd)
-    f8 = getattr(blk.bn2, "_cn_fp8", None)
+    f8 = fp8_of(blk.bn2)
     dc2, dg2, db2 = dgrad_bn_bwd(dc3, n, oh, ow, w3t, planes, 1, 0, 1, c2, st2[0], blk.bn2, grads,
                                  weight=blk.conv3.weight, ctx=f8)
     # configs[4]: e5m2 dc2 (shared with conv2's fp8 dgrad below) x the forward's e4m3 y1
@@ -410,7 +431,7 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     # fp8 mode: the concat's e4m3 copy for the bottleneck conv, written by the branches' applies
     # (one delayed-scaling state for the whole concat; the pooled slice by a quantise pass)
     cat8 = qst = None
-    ctx = getattr(mod, "_cn_fp8", None) if dt == torch.bfloat16 else None
+    ctx = fp8_of(mod) if dt == torch.bfloat16 else None
     if ctx is not None:
         qst = ctx.acts.ready(("cat", id(mod)), dev)
         if qst is not None:
@@ -455,7 +476,7 @@ def aspp_bwd(item, dout, grads):
     x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, q8s, qb = sv
     hw = h * w
     P = n * hw
-    f8 = getattr(mod.bn, "_cn_fp8", None)
+    f8 = fp8_of(mod.bn)
     use8 = f8 is not None and WGRAD_FP8
     x, cat, cb, out = x[:P], cat[:P], cb[:P], out[:P]
     pool, cp, yp = pool[:n], cp[:n], yp[:n]

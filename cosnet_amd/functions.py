@@ -49,206 +49,89 @@ def _check_train(ctx):
 
 
 # ==============================================================================================
+# The per-module encoder blocks (frames of different sizes: the model's unpaired path, e.g.
+# configs[3]'s 1 target vs 5 references).  Each is an autograd wrapper over the SAME block
+# functions the paired encoder pass runs (encoder_fn.stem_fwd / bottleneck_fwd / aspp_fwd and
+# their backwards) with one frame segment and bf16 / fp32 operands, so the two paths cannot
+# drift apart (tests/test_gpu_blocks_bf16.py::test_per_module_blocks_are_the_paired_code).
+def _enc():
+    from . import encoder_fn   # encoder_fn imports this module (F, _GRAD)
+    return encoder_fn
+
+
 class StemFn(F):
     @staticmethod
     def forward(ctx, img, mod, w, g, b):
-        n, cimg, h, wd = img.shape
+        E = _enc()
         dt = getattr(mod, "_cn_dtype", torch.bfloat16)
-        x = torch.empty((n * h * wd, 8), dtype=dt, device=img.device)
-        nv.call("cn_nchw_to_nhwc", nv.dtype_code(dt), img.data_ptr(), n, cimg, h, wd, 8,
-                x.data_ptr(), nv.stream())
-        wf, _ = WCACHE.get(w, dt, cin_pad=8, need_t=False)
-        c, oh, ow = conv_fwd(x, n, h, wd, wf, 64, 7, 2, 3, 1)
-        st = bn_stats(c, mod.bn1, mod.training)
-        y = bn_apply(c, st, mod.bn1, act=1)
-        ph, pw = ops.pool_out(oh), ops.pool_out(ow)
-        out = torch.empty((n * ph * pw, 64), dtype=dt, device=img.device)
-        am = torch.empty((n * ph * pw * 64,), dtype=torch.uint8, device=img.device)
-        nv.call("cn_maxpool_fwd", nv.dtype_code(dt), y.data_ptr(), n, oh, ow, 64, ph, pw, 3, 2, 1,
-                out.data_ptr(), am.data_ptr(), nv.stream())
-        if _need(ctx):
-            ctx.s = (x, c, y, am, st)
-        ctx.geo = (n, cimg, h, wd, oh, ow, ph, pw)
-        ctx.mod = mod
+        rec = [] if _need(ctx) else None
+        with E.no_fp8():
+            out, _ = E.stem_fwd(mod, (img,), 1, dt, rec)
+        ctx.item = rec[0] if rec else None
+        ctx.params = (w, g, b)
         ctx.training = mod.training
         return out
 
     @staticmethod
     def backward(ctx, dout):
         _check_train(ctx)
-        x, c, y, am, st = ctx.s
-        n, cimg, h, wd, oh, ow, ph, pw = ctx.geo
-        dout = dout.contiguous()
-        dy = torch.empty_like(y)
-        nv.call("cn_maxpool_bwd", ops.dtc(dout), dout.data_ptr(), am.data_ptr(), n, oh, ow, 64, ph,
-                pw, 3, 2, 1, dy.data_ptr(), nv.stream())
-        dc, dg, db, _ = bn_bwd(c, dy, None, st, ctx.mod.bn1, act=1)
-        dw = conv_wgrad(x, n, h, wd, 8, dc, oh, ow, 64, 7, 2, 3, 1)
-        dw = dw.view(64, 7, 7, 8)[..., :cimg].permute(0, 3, 1, 2)
-        return None, None, dw, dg, db
+        E = _enc()
+        grads = E.GradSink()
+        with E.no_fp8():
+            E.stem_bwd(ctx.item, dout if dout.stride(1) == 1 else dout.contiguous(), grads)
+        ctx.item = None
+        return (None, None) + tuple(grads.get(p) for p in ctx.params)
 
 
 # ==============================================================================================
 class BottleneckFn(F):
     @staticmethod
     def forward(ctx, x, blk, geo, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd):
-        n, h, w = geo
-        dt = x.dtype
-        tr = blk.training
-        s, d = blk.stride, blk.dilation
-        planes = w1.shape[0]
-        w1f, w1t = WCACHE.get(w1, dt)
-        w2f, w2t = WCACHE.get(w2, dt)
-        w3f, w3t = WCACHE.get(w3, dt)
-        c1, oh, ow = conv_fwd(x, n, h, w, w1f, planes, 1, s, 0, 1)
-        st1 = bn_stats(c1, blk.bn1, tr)
-        y1 = bn_apply(c1, st1, blk.bn1, act=1)
-        c2, _, _ = conv_fwd(y1, n, oh, ow, w2f, planes, 3, 1, d, d)
-        st2 = bn_stats(c2, blk.bn2, tr)
-        y2 = bn_apply(c2, st2, blk.bn2, act=1)
-        c3, _, _ = conv_fwd(y2, n, oh, ow, w3f, 4 * planes, 1, 1, 0, 1)
-        st3 = bn_stats(c3, blk.bn3, tr)
-        cd = std = wdf = wdt = None
-        if wd is not None:
-            wdf, wdt = WCACHE.get(wd, dt)
-            bnd = blk.downsample[1]
-            cd, _, _ = conv_fwd(x, n, h, w, wdf, 4 * planes, 1, s, 0, 1)
-            std = bn_stats(cd, bnd, tr)
-            y = bn_apply(c3, st3, blk.bn3, act=1, xr=cd, rstats=std, rbn=bnd)
-        else:
-            y = bn_apply(c3, st3, blk.bn3, act=1, res=x)
-        if _need(ctx):
-            ctx.s = (x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt)
-        ctx.geo = (n, h, w, oh, ow, s, d, planes, x.shape[1])
-        ctx.blk = blk
-        ctx.training = tr
+        E = _enc()
+        rec = [] if _need(ctx) else None
+        with E.no_fp8():
+            y, _ = E.bottleneck_fwd(blk, x, geo, 1, rec)
+        ctx.item = rec[0] if rec else None
+        ctx.params = (w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd)
+        ctx.training = blk.training
         return y
 
     @staticmethod
     def backward(ctx, dy):
         _check_train(ctx)
-        x, c1, y1, c2, y2, c3, cd, y, st1, st2, st3, std, w1t, w2t, w3t, wdt = ctx.s
-        n, h, w, oh, ow, s, d, planes, cin = ctx.geo
-        blk = ctx.blk
-        dy = dy if dy.stride(1) == 1 else dy.contiguous()
-        has_down = cd is not None
+        E = _enc()
+        grads = E.GradSink()
         need_dx = ctx.needs_input_grad[0]
-        dx = None
-        if has_down:
-            dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3, blk.bn3, act=1)
-            dcd, _, _, _ = bn_bwd(cd, dy, y, std, blk.downsample[1], act=1)
-        else:
-            dx = torch.empty_like(x)
-            dc3, dg3, db3, _ = bn_bwd(c3, dy, y, st3, blk.bn3, act=1, dres=dx)
-        dw3 = conv_wgrad(y2, n, oh, ow, planes, dc3, oh, ow, 4 * planes, 1, 1, 0, 1)
-        dy2 = conv_dgrad(dc3, n, oh, ow, w3t, planes, 1, 1, 0, 1, oh, ow)
-        dc2, dg2, db2, _ = bn_bwd(c2, dy2, None, st2, blk.bn2, act=1)
-        dw2 = conv_wgrad(y1, n, oh, ow, planes, dc2, oh, ow, planes, 3, 1, d, d)
-        dy1 = conv_dgrad(dc2, n, oh, ow, w2t, planes, 3, 1, d, d, oh, ow)
-        dc1, dg1, db1, _ = bn_bwd(c1, dy1, None, st1, blk.bn1, act=1)
-        dw1 = conv_wgrad(x, n, h, w, cin, dc1, oh, ow, planes, 1, s, 0, 1)
-        dwd = None
-        if need_dx:
-            dx = conv_dgrad(dc1, n, oh, ow, w1t, cin, 1, s, 0, 1, h, w, out=dx, accumulate=dx is not None)
-        if has_down:
-            dwd = conv_wgrad(x, n, h, w, cin, dcd, oh, ow, 4 * planes, 1, s, 0, 1)
-            if need_dx:
-                conv_dgrad(dcd, n, oh, ow, wdt, cin, 1, s, 0, 1, h, w, out=dx, accumulate=True)
-        W = (blk.conv1.weight, blk.conv2.weight, blk.conv3.weight)
-        gdw = as_param_grad(dwd, blk.downsample[0].weight) if has_down else None
-        return (dx if need_dx else None, None, None,
-                as_param_grad(dw1, W[0]), dg1, db1, as_param_grad(dw2, W[1]), dg2, db2,
-                as_param_grad(dw3, W[2]), dg3, db3, gdw, None, None)
+        with E.no_fp8():
+            dx = E.bottleneck_bwd(ctx.item, dy if dy.stride(1) == 1 else dy.contiguous(), grads,
+                                  need_dx=need_dx)
+        ctx.item = None
+        return ((dx if need_dx else None), None, None) + tuple(
+            grads.get(p) if p is not None else None for p in ctx.params)
 
 
 # ==============================================================================================
 class ASPPFn(F):
     @staticmethod
     def forward(ctx, x, mod, geo, *p):
-        (wc, bc, gx, bx, w0, b0, g0, be0, w1, b1, g1, be1, w2, b2, g2, be2, w3, b3, g3, be3,
-         wb, bb, gb, beb, pw) = p
-        n, h, w = geo
-        hw = h * w
-        P = n * hw
-        dt = x.dtype
-        tr = mod.training
-        dev = x.device
-        cat = torch.empty((P, 2560), dtype=dt, device=dev)
-        pool = torch.empty((n, 2048), dtype=dt, device=dev)
-        ops.avgpool(x, n, hw, 1.0 / hw, pool)
-        wcf, wct = WCACHE.get(wc, dt)
-        cp, _, _ = conv_fwd(pool, n, 1, 1, wcf, 512, 1, 1, 0, 1, bias=bc)
-        stp = bn_stats(cp, mod.bn_x, tr)
-        yp = bn_apply(cp, stp, mod.bn_x, act=1)
-        nv.call("cn_bcast_rows", ops.dtc(yp), yp.data_ptr(), n, hw, 512, 1.0, cat.data_ptr(), 2560, 0,
-                nv.stream())
-        convs = [(mod.conv2d_0, mod.bn_0, w0, b0, 1, 0)]
-        for i, dd in enumerate(mod.cn_dilations):
-            convs.append((getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)),
-                          (w1, w2, w3)[i], (b1, b2, b3)[i], 3, dd))
-        cs, sts, wts = [], [], []
-        for bi, (cm, bnm, wi, bi_, k, dd) in enumerate(convs):
-            wf, wt = WCACHE.get(wi, dt)
-            ci, _, _ = conv_fwd(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bias=bi_)
-            st = bn_stats(ci, bnm, tr)
-            bn_apply(ci, st, bnm, act=1, out=cat[:, 512 * (bi + 1):512 * (bi + 2)])
-            cs.append(ci)
-            sts.append(st)
-            wts.append(wt)
-        wbf, wbt = WCACHE.get(wb, dt)
-        cb, _, _ = conv_fwd(cat, n, h, w, wbf, 256, 3, 1, 1, 1, bias=bb)
-        stb = bn_stats(cb, mod.bn, tr)
-        out = bn_apply(cb, stb, mod.bn, act=2, prelu=pw)
-        if _need(ctx):
-            ctx.s = (x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, pw)
-        ctx.geo = (n, h, w)
-        ctx.mod = mod
-        ctx.training = tr
-        ctx.convs = [(k, dd) for (_, _, _, _, k, dd) in convs]
+        E = _enc()
+        rec = [] if _need(ctx) else None
+        with E.no_fp8():
+            out = E.aspp_fwd(mod, x, geo, 1, rec)
+        ctx.item = rec[0] if rec else None
+        ctx.params = p
+        ctx.training = mod.training
         return out
 
     @staticmethod
     def backward(ctx, dout):
         _check_train(ctx)
-        x, pool, cp, yp, stp, wct, cs, sts, wts, cat, cb, stb, wbt, out, pw = ctx.s
-        n, h, w = ctx.geo
-        hw = h * w
-        mod = ctx.mod
-        dout = dout if dout.stride(1) == 1 else dout.contiguous()
-        dcb, dgb, dbb, dpr = bn_bwd(cb, dout, out, stb, mod.bn, act=2, prelu=pw)
-        dwb = conv_wgrad(cat, n, h, w, 2560, dcb, h, w, 256, 3, 1, 1, 1)
-        dbias_b = ops.colsum(dcb)
-        dcat = conv_dgrad(dcb, n, h, w, wbt, 2560, 3, 1, 1, 1, h, w)
-        need_dx = ctx.needs_input_grad[0]
-        dx = None
-        grads = []
-        bns = [mod.bn_0, mod.bn_1, mod.bn_2, mod.bn_3]
-        for bi, ((k, dd), ci, st, wt) in enumerate(zip(ctx.convs, cs, sts, wts)):
-            sl = slice(512 * (bi + 1), 512 * (bi + 2))
-            dci, dgi, dbi, _ = bn_bwd(ci, dcat[:, sl], None, st, bns[bi], act=1)
-            dwi = conv_wgrad(x, n, h, w, 2048, dci, h, w, 512, k, 1, dd, max(dd, 1))
-            dbias = ops.colsum(dci)
-            if need_dx:
-                dx = conv_dgrad(dci, n, h, w, wt, 2048, k, 1, dd, max(dd, 1), h, w, out=dx,
-                                accumulate=dx is not None)
-            grads.append((dwi, dbias, dgi, dbi))
-        # image-pool branch: sum over HW of its cat slice
-        dyp = torch.empty((n, 512), dtype=dout.dtype, device=dout.device)
-        ops.avgpool(dcat[:, :512], n, hw, 1.0, dyp)
-        dcp, dgx, dbx, _ = bn_bwd(cp, dyp, None, stp, mod.bn_x, act=1)
-        dwc = conv_wgrad(pool, n, 1, 1, 2048, dcp, 1, 1, 512, 1, 1, 0, 1)
-        dbc = ops.colsum(dcp)
-        if need_dx:
-            dpool = conv_dgrad(dcp, n, 1, 1, wct, 2048, 1, 1, 0, 1, 1, 1)
-            nv.call("cn_bcast_rows", ops.dtc(dpool), dpool.data_ptr(), n, hw, 2048, 1.0 / hw,
-                    dx.data_ptr(), ops.ld(dx), 1, nv.stream())
-        convmods = [mod.conv2d_0, mod.conv2d_1, mod.conv2d_2, mod.conv2d_3]
-        res = [dx if need_dx else None, None, None,
-               as_param_grad(dwc, mod.conv.weight), dbc, dgx, dbx]
-        for (dwi, dbias, dgi, dbi), cm in zip(grads, convmods):
-            res += [as_param_grad(dwi, cm.weight), dbias, dgi, dbi]
-        res += [as_param_grad(dwb, mod.bottleneck.weight), dbias_b, dgb, dbb, dpr]
-        return tuple(res)
+        E = _enc()
+        grads = E.GradSink()
+        with E.no_fp8():
+            dx = E.aspp_bwd(ctx.item, dout if dout.stride(1) == 1 else dout.contiguous(), grads)
+        ctx.item = None
+        return (dx if ctx.needs_input_grad[0] else None, None, None) + tuple(grads.get(q) for q in ctx.params)
 
 
 # ==============================================================================================

@@ -24,10 +24,13 @@ Data parallel (world > 1): every gradient lives in one flat fp32 "arena", cut in
 layer3 (halves for the RGB encoder), [layer2 + layer1 + stem]).  The encoder backwards are
 deferred out of autograd (encoder_fn.DeferredEncoderBwd) and write their gradients straight
 into their bucket, so nothing is packed.  Each segment is one graph on its encoder's stream, and
-its bucket's all-reduce (RCCL, async, pre-scaled by 1/world and summed = DataParallel's mean) is
+its bucket's all-reduce (RCCL, async, ReduceOp.AVG = DataParallel's mean; gloo: pre-scaled by
+1/world and summed) is
 issued on the host as soon as that graph is queued: bucket k reduces over xGMI while the later
 segments compute.  Optionally the buckets are reduced in bf16 (grad_dtype="bf16": half the
-bytes).  dp_chain=True runs the same chain at world 1 without collectives (timing / tracing).
+bytes).  dp_chain=True runs the same chain at world 1 without collectives (timing / tracing);
+collectives=True keeps the collectives at world 1 on an initialised process group (a world-1 RCCL
+communicator is legal on one device: configs[2]'s per-rank step with RCCL really in the chain).
 BN running statistics stay per rank during training (train-mode BN normalises with batch
 statistics, so they never enter the step); sync_buffers() broadcasts rank 0's before evaluation
 or checkpointing.
@@ -46,7 +49,7 @@ class TrainStep:
     """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
 
     def __init__(self, model, opt, batch, size, l1_weight=0.8, graphed=True, group=None,
-                 grad_dtype="fp32", split_graphs=None, dp_chain=None):
+                 grad_dtype="fp32", split_graphs=None, dp_chain=None, collectives=None):
         self.model, self.opt = model, opt
         # split_graphs (encoders on two streams): record the step as one-stream graphs per phase
         # and stream (_program) instead of one graph with a forked branch.  ROCm's launch of a
@@ -67,7 +70,16 @@ class TrainStep:
         # traced on one GPU (bench.py --dp-chain 1).  CN_DP_CHAIN=1 sets it.
         if dp_chain is None:
             dp_chain = os.environ.get("CN_DP_CHAIN", "0") == "1"
-        self.dp_mode = self.world > 1 or bool(dp_chain)
+        # collectives: issue the positive-count and bucket all-reduces even at world 1 (needs an
+        # initialised process group, e.g. a world-1 "nccl" group = RCCL on this one device);
+        # CN_DP_COLLECTIVES=1 sets it.  At world > 1 they are always issued.
+        if collectives is None:
+            collectives = os.environ.get("CN_DP_COLLECTIVES", "0") == "1"
+        dist_on = dist.is_available() and dist.is_initialized()
+        if collectives and not dist_on:
+            raise RuntimeError("collectives=True needs an initialised torch.distributed process group")
+        self.coll = self.world > 1 or (bool(collectives) and dist_on)
+        self.dp_mode = self.world > 1 or bool(dp_chain) or self.coll
         dev = next(model.parameters()).device
         b = batch
         h, w = (size, size) if isinstance(size, int) else tuple(size)
@@ -111,7 +123,7 @@ class TrainStep:
         """Global #(gt >= 0.5) of both frames (train.py:183-187), before the graph."""
         fn.count_positive(self.gt_a, out=self.cnt[0:1])
         fn.count_positive(self.gt_b, out=self.cnt[1:2])
-        if self.world > 1:
+        if self.coll:
             dist.all_reduce(self.cnt, group=self.group)
 
     def _mem(self, prefix):
@@ -262,10 +274,13 @@ class TrainStep:
                     op[2]()
             else:
                 self._host_op(op, S)
-        # tensors handed across the streams stay alive in `env` until every piece has run (the
-        # final join orders both streams before SGD); nothing is freed while the other stream uses it
+        # The step's tensors are released here, once every piece is queued: a block returns to
+        # the pool of the stream it was allocated on, and its next user there is ordered after
+        # the other stream's use of it -- an s1 tensor read on s2 by the final join (s1 waits for
+        # s2 before SGD), an s2 tensor read on s1 by the next step's first join (s2 waits for s1).
+        # (Kept alive until the next step, they raised the eager path's peak by one step's env.)
         self.loss = env["loss"]
-        self._env_eager = env
+        env.clear()
 
     def _record_program(self):
         """Record each piece as one graph on its stream; a memory pool per stream, so a graph never
@@ -360,7 +375,8 @@ class TrainStep:
             half = torch.zeros((n,), dtype=torch.bfloat16, device=dev)
         self.dp = {"buckets": buckets, "ranges": ranges, "pieces": pieces, "flat": flat,
                    "arena": arena, "views": views, "half": half, "works": [],
-                   "head_live": [None, None], "defers": defers}
+                   "head_live": [None, None], "defers": defers, "issued": 0,
+                   "avg": bool(getattr(self, "coll", False)) and dist.get_backend(self.group) == "nccl"}
         self.flat = flat
 
     def _dp_head_bucket(self, k):
@@ -382,24 +398,31 @@ class TrainStep:
 
     def _dp_prepare_bucket(self, k):
         """Device work that readies bucket k for its all-reduce: the 1/world pre-scale (sum of
-        scaled = DataParallel's mean) and, for bf16 reduction, the cast."""
+        scaled = DataParallel's mean) and, for bf16 reduction, the cast.  On RCCL the bucket is
+        reduced with ReduceOp.AVG instead: RCCL applies the 1/world factor inside its reduction
+        kernel (a pre-multiplied sum), so the separate read + write pass over the 570 MB of
+        gradients per step is gone; gloo has no AVG and keeps the pre-scale."""
         dp = self.dp
         a, b = dp["ranges"][k]
         if b == a:
             return
-        nv.call("cn_scale", dp["flat"][a:].data_ptr(), b - a, 1.0 / self.world, nv.stream())
+        if not dp["avg"]:
+            nv.call("cn_scale", dp["flat"][a:].data_ptr(), b - a, 1.0 / self.world, nv.stream())
         if dp["half"] is not None:
             ops.cast_copy(dp["flat"][a:b].view(-1, 1), dp["half"][a:b].view(-1, 1))
 
     def _dp_launch_reduce(self, k):
         """Issue bucket k's all-reduce (async): RCCL waits for the work queued so far on the
-        current stream and runs beside the pieces queued after it.  World 1 (forced chain): none."""
+        current stream and runs beside the pieces queued after it.  World 1 without collectives
+        (forced chain): none."""
         dp = self.dp
         a, b = dp["ranges"][k]
-        if b == a or self.world == 1:
+        if b == a or not self.coll:
             return
         buf = dp["half"][a:b] if dp["half"] is not None else dp["flat"][a:b]
-        dp["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
+        op = dist.ReduceOp.AVG if dp["avg"] else dist.ReduceOp.SUM
+        dp["works"].append(dist.all_reduce(buf, op=op, group=self.group, async_op=True))
+        dp["issued"] += 1
 
     def _dp_sgd(self):
         """(Cast the reduced bf16 buckets back,) point the parameters' .grad at the arena, SGD."""

@@ -36,6 +36,7 @@ def _worker(rank, world, port, q):
         g0, g1 = reference_param_groups(m)
         ts = TrainStep.__new__(TrainStep)        # the planning half only (no device tables)
         ts.model, ts.group, ts.world, ts.grad_dtype = m, None, world, "fp32"
+        ts.coll = True     # world > 1 (or world 1 with TrainStep collectives=True)
         seen, ts.params = set(), []
         for p in list(g0) + list(g1):
             if id(p) not in seen:
@@ -69,14 +70,15 @@ def _worker(rank, world, port, q):
             w.wait()
         a, b = dp["ranges"][0][0], dp["ranges"][-1][1]
         red = dp["flat"][a:b]
+        nb = sum(1 for a_, b_ in dp["ranges"] if b_ > a_)
+        ok_stage &= dp["issued"] == nb
         q.put((rank, ok_cover, ok_align, ok_contig, ok_alias, ok_stage, len(dp["pieces"]),
                float(red.min()), float(red.max())))
     finally:
         dist.destroy_process_group()
 
 
-def test_bucket_plan_and_reduction_two_ranks():
-    world = 2
+def _run(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -90,4 +92,28 @@ def test_bucket_plan_and_reduction_two_ranks():
     for rank, cover, align, contig, alias, stage, nseg, lo, hi in res:
         assert cover and align and contig and alias and stage, (rank, cover, align, contig, alias, stage)
         assert nseg == 7          # RGB: ASPP+layer4, layer3 x2, layer2+1+stem; depth: 3 of them
-        assert lo == hi == 1.5, (lo, hi)
+        want = sum(r + 1 for r in range(world)) / world
+        assert lo == hi == want, (lo, hi)
+
+
+def test_bucket_plan_and_reduction_two_ranks():
+    _run(2)
+
+
+def test_bucket_reduction_world1_collectives():
+    """World 1 with collectives on (bench.py --dp-chain 1 --dist-backend nccl issues the same
+    calls on a world-1 RCCL group): every non-empty bucket's all-reduce is really issued."""
+    _run(1)
+
+
+def test_collectives_need_a_process_group():
+    import pytest
+    import cosnet_amd as C
+    from cosnet_amd.optim import SGD, reference_param_groups
+    from cosnet_amd.train_step import TrainStep
+    if dist.is_initialized():
+        pytest.skip("process group present")
+    m = C.build_model(torch.float32)
+    g0, g1 = reference_param_groups(m)
+    with pytest.raises(RuntimeError, match="process group"):
+        TrainStep(m, SGD([g0, g1], [0.0, 0.0]), 2, 65, collectives=True)

@@ -196,3 +196,75 @@ def test_aspp_bf16_matches_fp64(cuda):
     for k in check:
         got[k] = grads[mods[k]].reshape(res[True][k].shape)
     _check("ASPP", got, res)
+
+
+def test_per_module_blocks_are_the_paired_code(cuda):
+    """The per-module path (functions.StemFn / BottleneckFn / ASPPFn: the model's unpaired
+    forward, e.g. configs[3]'s 1 target vs 5 references) is an autograd wrapper over the paired
+    pass's block functions: run with one frame segment, a bottleneck with a stride-2 downsample
+    (layer2[0]), an identity layer-3 bottleneck, the stem and the ASPP give BITWISE the outputs
+    and gradients of encoder_fn.*_fwd / *_bwd called directly -- one implementation, no drift."""
+    from cosnet_amd import functions as fn
+    m = _model(cuda)
+    m._set_dtype()
+    bb = m.encoder.backbone
+    g = torch.Generator().manual_seed(13)
+
+    def run_fn(cls, x, mod, geo, params):
+        xr = x.clone().requires_grad_(True)
+        ps = [p for p in params]
+        out = cls.apply(xr, mod, geo, *ps) if cls is not fn.StemFn else cls.apply(xr, mod, *ps)
+        return out, xr, ps
+
+    # bottlenecks
+    for blk, n, h, w, cin in ((bb.layer2[0], 2, 60, 60, 256), (bb.layer3[5], 2, 30, 30, 1024)):
+        x = torch.relu(torch.randn((n * h * w, cin), generator=g)).to(torch.bfloat16).to(cuda)
+        d = blk.downsample
+        params = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                  blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias,
+                  d[0].weight if d is not None else None, d[1].weight if d is not None else None,
+                  d[1].bias if d is not None else None]
+        y, xr, _ = run_fn(fn.BottleneckFn, x, blk, (n, h, w), params)
+        dy = (torch.randn(tuple(y.shape), generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+        live = [p for p in params if p is not None and p.requires_grad]
+        gf = torch.autograd.grad(y, [xr] + live, dy)
+        rec = []
+        y2, _ = E.bottleneck_fwd(blk, x, (n, h, w), 1, rec)
+        sink = E.GradSink()
+        dx2 = E.bottleneck_bwd(rec[0], dy, sink)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+        assert torch.equal(gf[0], dx2)
+        for p, gp in zip(live, gf[1:]):
+            assert torch.equal(gp, sink[p]), tuple(p.shape)
+    # stem
+    img = (torch.rand((2, 3, 97, 97), generator=g) * 255 - 110).to(cuda)
+    params = [bb.conv1.weight, bb.bn1.weight, bb.bn1.bias]
+    out = fn.StemFn.apply(img, bb, *params)
+    dout = (torch.randn(tuple(out.shape), generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    gf = torch.autograd.grad(out, params, dout)
+    rec = []
+    out2, _ = E.stem_fwd(bb, (img,), 1, torch.bfloat16, rec)
+    sink = E.GradSink()
+    E.stem_bwd(rec[0], dout, sink)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    for p, gp in zip(params, gf):
+        assert torch.equal(gp, sink[p]), tuple(p.shape)
+    # ASPP
+    mod = m.encoder.aspp
+    sc = torch.tensor([0.5, 1.5]).repeat_interleave(30 * 30)[:, None]
+    x = (torch.relu(torch.randn((2 * 30 * 30, 2048), generator=g)) * sc).to(torch.bfloat16).to(cuda)
+    params = mod._params()
+    out, xr, _ = run_fn(fn.ASPPFn, x, mod, (2, 30, 30), params)
+    dout = (torch.randn(tuple(out.shape), generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    gf = torch.autograd.grad(out, [xr] + params, dout)
+    rec = []
+    out2 = E.aspp_fwd(mod, x, (2, 30, 30), 1, rec)
+    sink = E.GradSink()
+    dx2 = E.aspp_bwd(rec[0], dout, sink)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    assert torch.equal(gf[0], dx2)
+    for p, gp in zip(params, gf[1:]):
+        assert torch.equal(gp, sink[p]), tuple(p.shape)

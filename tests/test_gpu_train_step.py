@@ -9,7 +9,7 @@ from cosnet_amd.optim import SGD, lr_poly, reference_param_groups
 from cosnet_amd.train_step import TrainStep
 
 
-def _setup(cuda, dtype, graphed, b=2, s=65, split=False, chain=False):
+def _setup(cuda, dtype, graphed, b=2, s=65, split=False, chain=False, coll=False):
     torch.manual_seed(0)
     fp8 = dtype == "fp8"
     m = C.build_model(torch.bfloat16 if fp8 else dtype)
@@ -20,7 +20,7 @@ def _setup(cuda, dtype, graphed, b=2, s=65, split=False, chain=False):
     m = m.to(cuda).train()
     g0, g1 = reference_param_groups(m)
     opt = SGD([g0, g1], [0.0, 0.0])
-    st = TrainStep(m, opt, b, s, graphed=graphed, split_graphs=split, dp_chain=chain)
+    st = TrainStep(m, opt, b, s, graphed=graphed, split_graphs=split, dp_chain=chain, collectives=coll)
     st.load(*[t.to(cuda) for t in synthetic_inputs(b, s, s, seed=5)])
     return m, st
 
@@ -102,6 +102,51 @@ def test_dp_chain_tracks_single_process_step(cuda, dtype):
     num = sum(float((x - y).double().square().sum()) for x, y in zip(b0, b1))
     den = sum(float(x.double().square().sum()) for x in b0)
     assert (num / den) ** 0.5 <= (1e-3 if dtype == torch.float32 else 5e-2), (num / den) ** 0.5
+
+
+@pytest.mark.gpu
+def test_rccl_world1_chain_tracks_single_process_step_473(cuda):
+    """configs[2]'s per-rank step (473x473, 4 pairs, bf16, recorded) through a REAL RCCL
+    communicator: a world-1 "nccl" process group, the positive-count all-reduce and every
+    bucket's async all-reduce issued from its piece's stream between the graph replays and
+    waited on before SGD (TrainStep collectives=True) -- against the single-process step, with
+    the bounds of test_dp_chain_tracks_single_process_step (bf16)."""
+    import socket
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, world_size=1, rank=0,
+                            device_id=cuda)
+    try:
+        assert dist.get_backend() == "nccl"
+        runs = [_setup(cuda, torch.bfloat16, graphed=True, b=4, s=473, split=True, chain=c, coll=c)
+                for c in (False, True)]
+        single, chain = runs[0][1], runs[1][1]
+        assert not single.coll and chain.coll and chain.dp_mode and chain.world == 1
+        for _, st in runs:
+            st.opt.set_lrs(_lrs(0))
+            st.capture(warmup=1)
+        assert chain._rec is not None and any(op[0] == "reduce" for op in chain._rec)
+        issued0 = chain.dp["issued"]
+        losses = [[float(st(_lrs(1 + i))) for i in range(2)] for _, st in runs]
+        torch.cuda.synchronize()
+        nb = sum(1 for a, b in chain.dp["ranges"] if b > a)
+        assert chain.dp["issued"] - issued0 == 2 * nb, (chain.dp["issued"], issued0, nb)
+        assert chain.dp["works"] == []
+        for a, b in zip(*losses):
+            assert abs(a - b) <= 2e-2 * abs(a), losses
+        b0, b1 = _bufs(single), _bufs(chain)
+        assert len(b0) == len(b1) > 300
+        num = sum(float((x - y).double().square().sum()) for x, y in zip(b0, b1))
+        den = sum(float(x.double().square().sum()) for x in b0)
+        assert (num / den) ** 0.5 <= 5e-2, (num / den) ** 0.5
+        assert all(torch.isfinite(x).all() for x in b1)
+    finally:
+        dist.destroy_process_group()
 
 
 @pytest.mark.gpu
