@@ -643,6 +643,10 @@ void coatt_q48_k(FusedArgs a) {
 
 }  // namespace
 
+__global__ __launch_bounds__(256) void q48_zero_cnt_k(int* cnt, int n) {
+  for (int i = threadIdx.x; i < n; i += 256) cnt[i] = 0;
+}
+
 int coatt_q48_rows() { return RB; }
 
 // Workgroups and partial slots per item for `items` items of `ntiles` key tiles: 256 ranges
@@ -684,8 +688,10 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
     a.opart = (float*)ws;                  // bf16 rows of FD channels
     a.mlpart = a.opart + rows * FD / 2;
     a.cnt = (int*)(a.mlpart + rows * 2);
-    const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)a.nitems * sizeof(int), st);
-    if (e != hipSuccess) return (int)e;
+    // zeroed by a kernel, not hipMemsetAsync: inside a recorded step that is a kernel node like
+    // every other (no memset nodes in the captured graphs); the merge resets each counter too
+    hipLaunchKernelGGL(q48_zero_cnt_k, dim3(1), dim3(256), 0, st, a.cnt, a.nitems);
+    CN_CHECK_LAUNCH();
   }
   if (mode == 0) hipLaunchKernelGGL(coatt_q48_k<0>, dim3(a.nwork), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(coatt_q48_k<1>, dim3(a.nwork), dim3(256), 0, st, a);

@@ -336,7 +336,8 @@ def bottleneck_fwd(blk, x, geo, nseg, rec):
     c1, oh, ow, st1 = conv_bn(x, n, h, w, w1f, planes, 1, s, 0, 1, blk.bn1, tr, nseg,
                               weight=blk.conv1.weight)
     y1 = c1 if _PROBE_SKIP & 1 else seg_apply(c1, st1, blk.bn1, act=1, fp8_key=id(blk.conv2.weight))
-    q2 = [] if rec is not None else None
+    # the e4m3 input copy is kept for the backward only when the fp8 weight gradient reads it
+    q2 = [] if rec is not None and WGRAD_FP8 else None
     c2, _, _, st2 = conv_bn(y1, n, oh, ow, w2f, planes, 3, 1, d, d, blk.bn2, tr, nseg,
                             weight=blk.conv2.weight, q8=q2)
     y2 = c2 if _PROBE_SKIP & 2 else seg_apply(c2, st2, blk.bn2, act=1, fp8_key=id(blk.conv3.weight))
@@ -443,7 +444,7 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     cs, sts, wts, q8s = [], [], [], []
     for bi, (cm, bnm, k, dd) in enumerate(convs):
         wf, wt = WCACHE.get(cm.weight, dt)
-        q = [] if rec is not None else None
+        q = [] if rec is not None and WGRAD_FP8 else None
         ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias,
                                weight=cm.weight, q8=q)
         q8s.append(q)
@@ -461,7 +462,7 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     elif ctx is not None:
         ctx.acts.quant(cat, ("cat", id(mod)))   # first use: calibrates the concat's scale
     wbf, wbt = WCACHE.get(mod.bottleneck.weight, dt)
-    qb = [] if rec is not None else None
+    qb = [] if rec is not None and WGRAD_FP8 else None
     cb, _, _, stb = conv_bn(cat, n, h, w, wbf, 256, 3, 1, 1, 1, mod.bn, tr, nseg, bias=mod.bottleneck.bias,
                             weight=mod.bottleneck.weight, q8=qb)
     out = seg_apply(cb, stb, mod.bn, act=2, prelu=mod.prelu.weight)

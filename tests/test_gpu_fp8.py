@@ -159,3 +159,72 @@ def test_fp8_weight_gradient_of_bottleneck_matches_its_operands(cuda, monkeypatc
     e16 = ((dw2 - ref16).norm() / ref16.norm()).item()
     assert e16 <= qerr + 2e-3, (e16, qerr)
     ctx.grads.end()
+
+
+def test_fp8_vs_bf16_weight_gradient_with_pinned_scales(cuda, monkeypatch):
+    """The bf16-vs-fp8 weight-gradient comparison of round 5's two-pass test, restored with the
+    scale states pinned.  That test ran the block twice on one fp8 context (conv2's weight
+    gradient fp8, then bf16) and failed at 0.166 against its bound 1.25 x 0.073 + 0.02
+    (gpurun_out/r5d/01_tests.log:398): between the passes the context's delayed scales had
+    moved -- Fp8Acts.end() / grads.end() of pass 1 advanced every activation and gradient scale,
+    and pass 1 had CALIBRATED them (a first use quantises with the tensor's own amax) while pass
+    2 quantised with the advanced delayed scales -- so pass 2's forward fp8 convs, its fp8
+    dgrads and hence its y1 and dc2 were different operands, and the comparison measured two
+    independent fp8 quantisations of the whole block, not the weight gradient's precision.  Here
+    both passes start from the same fresh scale state (as pass 1 did), so y1 and dc2 are bitwise
+    equal across them and the two weight gradients differ only by conv2's operand format:
+    |fp8 - bf16| <= the operand quantisation distance measured on these operands + 2e-3."""
+    from cosnet_amd import encoder_fn as E
+    n1, h, w = 4, 60, 60
+    m = C.build_model(torch.bfloat16)
+    m.load_state_dict(recipe_state_dict(m.state_dict()))
+    m = m.to(cuda).train()
+    m.set_fp8(True)
+    m._set_dtype()
+    ctx = m.fp8
+    blk = m.encoder.backbone.layer3[5]
+    g = torch.Generator().manual_seed(21)
+    x = torch.relu(torch.randn((2 * n1 * h * w, 1024), generator=g)).to(torch.bfloat16).to(cuda)
+    dy = (torch.randn((n1 * h * w, 1024), generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    out = {}
+    for on in (True, False):
+        for a in (ctx.acts, ctx.grads):   # pin: every pass starts from the same (fresh) scales
+            a.states, a.slots, a.calibrated, a.pass_cache = None, {}, set(), {}
+        monkeypatch.setattr(E, "WGRAD_FP8", on)
+        ctx.acts.begin()
+        rec = []
+        E.bottleneck_fwd(blk, x, (2 * n1, h, w), 2, rec)
+        ctx.acts.end()
+        ctx.grads.begin()
+        grads, wq = E.GradSink(), E.WgradQueue()
+        E.bottleneck_bwd(rec[0], dy, grads, wq=wq)
+        wq.flush()
+        torch.cuda.synchronize()
+        dys = [v for v in ctx.grads.pass_cache.values() if tuple(v[0].shape) == (n1 * h * w, 256)]
+        assert len(dys) == 1
+        out[on] = (grads[blk.conv2.weight].detach().double().cpu(), rec[0][2][2][:n1 * h * w].clone(),
+                   dys[0][2].clone(), rec[0][2][16][0] if on else None, dys[0][0].clone(),
+                   dys[0][1][0].item())
+        ctx.grads.end()
+    (dw8, y1a, dca, q2, dy8, ds), (dw16, y1b, dcb, _, _, _) = out[True], out[False]
+    # the pinned scales reproduce the forward and the dgrad chain bit for bit
+    assert torch.equal(y1a, y1b) and torch.equal(dca, dcb)
+    x8, handle, slot = q2
+    sx = handle.state(slot)[0].item()
+
+    def wgrad64(xa, da):
+        xp = torch.nn.functional.pad(xa, (0, 0, 2, 2, 2, 2))
+        ref = torch.empty((256, 256, 3, 3), dtype=torch.float64)
+        for r in range(3):
+            for s in range(3):
+                ref[:, :, r, s] = da.t() @ xp[:, 2 * r:2 * r + h, 2 * s:2 * s + w, :].reshape(-1, 256)
+        return ref
+    ref8 = wgrad64(x8[:n1 * h * w].cpu().view(torch.float8_e4m3fn).double().view(n1, h, w, 256) * sx,
+                   dy8.cpu().view(torch.float8_e5m2).double().view(n1 * h * w, 256) * ds)
+    ref16 = wgrad64(y1a.double().cpu().view(n1, h, w, 256), dca.double().cpu())
+    qerr = ((ref8 - ref16).norm() / ref16.norm()).item()
+    e = ((dw8 - dw16).norm() / dw16.norm()).item()
+    e16 = ((dw16 - ref16).norm() / ref16.norm()).item()
+    print("fp8 vs bf16 weight gradient: %.4f, operand quantisation %.4f, bf16 vs fp64 %.2e" % (e, qerr, e16))
+    assert e16 <= 1e-2, e16                  # the bf16 weight gradient of these operands
+    assert 0 < e <= qerr + 2e-3 + e16, (e, qerr, e16)
