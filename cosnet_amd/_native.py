@@ -71,6 +71,8 @@ _SIGS = {
     "cn_coatt_fused_workspace_bytes": (_S, [_I, _I, _I]),
     "cn_coatt_f8_workspace_bytes": (_S, [_I, _I]),
     "cn_coatt_f8_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
+    "cn_coatt_f8_train_workspace_bytes": (_S, [_I, _I]),
+    "cn_coatt_f8_train_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _L, _P, _S, _P]),
     "cn_coatt_flash_fwd": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P]),
     "cn_coatt_flash_fwd_ws": (_I, [_P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _P, _L, _P, _P, _P, _S, _P]),
     "cn_coatt_flash_pv": (_I, [_P, _L, _P, _L, _P, _L, _P, _I, _I, _I, _P, _L, _I, _P]),

@@ -73,12 +73,27 @@ __device__ __forceinline__ unsigned pk4(float a, float b, float c, float d) {
 
 __device__ __forceinline__ float clampf8(float x) { return fminf(fmaxf(x, -F8MAX), F8MAX); }
 
+// e4m3 byte `sel` of a packed word -> float (exact)
+__device__ __forceinline__ float dec8(unsigned w, int sel) {
+  switch (sel) {
+    case 0: return __builtin_amdgcn_cvt_f32_fp8((int)w, 0);
+    case 1: return __builtin_amdgcn_cvt_f32_fp8((int)w, 1);
+    case 2: return __builtin_amdgcn_cvt_f32_fp8((int)w, 2);
+    default: return __builtin_amdgcn_cvt_f32_fp8((int)w, 3);
+  }
+}
+
 // ---- prepass: rows (Q / K images) ------------------------------------------------------------
 // thread = (row, 32-channel block); rows >= HW of each batch entry are zero
+// bexp (training, coatt_f8_blkexp_k): the exponent of the row's 32 x 32 block instead of the
+// row segment's own; dq (training): the decoded MX values as bf16 (exact: 3 mantissa bits times
+// a power of two), the operand the flash backward recomputes S from.
 __global__ __launch_bounds__(256) void coatt_f8_rows_k(const bf16* __restrict__ x, long long ldx,
                                                        int B, int HW, int HWp,
                                                        unsigned char* __restrict__ x8,
-                                                       unsigned char* __restrict__ xs) {
+                                                       unsigned char* __restrict__ xs,
+                                                       const unsigned char* __restrict__ bexp,
+                                                       bf16* __restrict__ dq, long long lddq) {
   const long long t = blockIdx.x * 256ll + threadIdx.x;
   if (t >= (long long)B * HWp * 8) return;
   const int bi = (int)(t & 7);
@@ -93,10 +108,15 @@ __global__ __launch_bounds__(256) void coatt_f8_rows_k(const bf16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 32; ++i) v[i] = 0.f;
   }
-  float amax = 0.f;
+  int e;
+  if (bexp) {
+    e = bexp[((long long)b * (HWp >> 5) + (r >> 5)) * 8 + bi];
+  } else {
+    float amax = 0.f;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
-  const int e = e8m0_of(amax);
+    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    e = e8m0_of(amax);
+  }
   const float inv = ldexpf(1.f, 127 - e);
   u32x4 o0, o1;
   unsigned w[8];
@@ -110,6 +130,45 @@ __global__ __launch_bounds__(256) void coatt_f8_rows_k(const bf16* __restrict__ 
   *(u32x4*)dst = o0;
   *(u32x4*)(dst + 16) = o1;
   xs[prow * 8 + 4 * (bi & 1) + (bi >> 1)] = (unsigned char)e;
+  if (dq && r < HW) {
+    const float sc = ldexpf(1.f, e - 127);
+    bf16* dd = dq + ((long long)b * HW + r) * lddq + 32 * bi;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = dec8(w[2 * q + (j >> 2)], j & 3) * sc;
+      *(u32x4*)(dd + 8 * q) = Chunk<bf16>::pack(f);
+    }
+  }
+}
+
+// Shared exponents for an operand used both as rows (S = Q K^T: blocks of 32 channels) and as V
+// (P V: blocks of 32 keys) -- Vb in training: one E8M0 exponent per 32 keys x 32 channels, so the
+// two MX images decode to the SAME values and the backward's single bf16 copy is the operand of
+// every product that read Vb.  One wave per block: lane -> key 2 x (lane >> 1) .. (16 channels).
+__global__ __launch_bounds__(256) void coatt_f8_blkexp_k(const bf16* __restrict__ x, long long ldx,
+                                                         int B, int HW, int nkb,
+                                                         unsigned char* __restrict__ bexp) {
+  const long long wv = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  if (wv >= (long long)B * nkb * 8) return;
+  const int lane = threadIdx.x & 63;
+  const int cb = (int)(wv & 7);
+  const long long bk = wv >> 3;
+  const int kb = (int)(bk % nkb), b = (int)(bk / nkb);
+  const int key = kb * 32 + (lane >> 1);
+  float amax = 0.f;
+  if (key < HW) {
+    const bf16* src = x + ((long long)b * HW + key) * ldx + 32 * cb + 16 * (lane & 1);
+    float v[16];
+    Chunk<bf16>::unpack(*(const u32x4*)src, v);
+    Chunk<bf16>::unpack(*(const u32x4*)(src + 8), v + 8);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if (lane == 0) bexp[wv] = (unsigned char)e8m0_of(amax);
 }
 
 // ---- prepass: V^T tiles ------------------------------------------------------------------------
@@ -118,7 +177,9 @@ __global__ __launch_bounds__(256) void coatt_f8_rows_k(const bf16* __restrict__ 
 // i = (kk & 3) + 4 (kk >> 3), i.e. key(h, j) above
 __global__ __launch_bounds__(256) void coatt_f8_vt_k(const bf16* __restrict__ v, long long ldv, int B,
                                                      int HW, int nt, unsigned char* __restrict__ vt8,
-                                                     unsigned char* __restrict__ vts) {
+                                                     unsigned char* __restrict__ vts,
+                                                     const unsigned char* __restrict__ bexp, int nkb,
+                                                     bf16* __restrict__ dq, long long lddq) {
   const long long t = blockIdx.x * 256ll + threadIdx.x;
   if (t >= (long long)B * nt * 2 * D) return;
   const int d = (int)(t % D);
@@ -132,11 +193,17 @@ __global__ __launch_bounds__(256) void coatt_f8_vt_k(const bf16* __restrict__ v,
     const int key = tile * KT + 32 * u + kk;
     x[kk] = key < HW ? (float)v[((long long)b * HW + key) * ldv + d] : 0.f;
   }
-  float amax = 0.f;
+  int e;
+  if (bexp) {
+    e = bexp[((long long)b * nkb + 2 * tile + u) * 8 + (d >> 5)];
+  } else {
+    float amax = 0.f;
 #pragma unroll
-  for (int kk = 0; kk < 32; ++kk) amax = fmaxf(amax, fabsf(x[kk]));
-  const int e = e8m0_of(amax);
+    for (int kk = 0; kk < 32; ++kk) amax = fmaxf(amax, fabsf(x[kk]));
+    e = e8m0_of(amax);
+  }
   const float inv = ldexpf(1.f, 127 - e);
+  const float sc = ldexpf(1.f, e - 127);
   // half h gets keys kk with (kk >> 2) & 1 == h, at byte 16u + (kk & 3) + 4 (kk >> 3)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -144,8 +211,17 @@ __global__ __launch_bounds__(256) void coatt_f8_vt_k(const bf16* __restrict__ v,
 #pragma unroll
     for (int i = 0; i < 16; ++i) y[i] = clampf8(x[(i & 3) + 8 * (i >> 2) + 4 * h] * inv);
     unsigned char* dst = vt8 + (bt * D + d) * KT + 32 * h + 16 * u;
-    *(u32x4*)dst = u32x4{pk4(y[0], y[1], y[2], y[3]), pk4(y[4], y[5], y[6], y[7]),
-                         pk4(y[8], y[9], y[10], y[11]), pk4(y[12], y[13], y[14], y[15])};
+    const u32x4 pw = u32x4{pk4(y[0], y[1], y[2], y[3]), pk4(y[4], y[5], y[6], y[7]),
+                           pk4(y[8], y[9], y[10], y[11]), pk4(y[12], y[13], y[14], y[15])};
+    *(u32x4*)dst = pw;
+    if (dq) {   // decoded value of key kk = (i & 3) + 8 (i >> 2) + 4 h at channel d
+      const unsigned wd[4] = {pw.x, pw.y, pw.z, pw.w};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = tile * KT + 32 * u + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (key < HW) dq[((long long)b * HW + key) * lddq + d] = (bf16)(dec8(wd[i >> 2], i & 3) * sc);
+      }
+    }
   }
   vts[bt * 512 + u * 256 + (d & 31) * 8 + (d >> 5)] = (unsigned char)e;
 }
@@ -377,6 +453,11 @@ extern "C" size_t cn_coatt_f8_workspace_bytes(int B, int HW) {
 
 // Z_a, Z_b (bf16) of the co-attention with MX-fp8 operands; lse_a / lse_b (optional, [B][HWp32],
 // HWp32 = ceil32(HW)) as cn_coatt_flash_fwd's, for the bf16 flash backward.
+static int f8_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                  const void* vb, long long ld_vb, int B, int HW, void* za, void* zb, long long ld_z,
+                  float* lse_a, float* lse_b, void* ws, bool train, void* vat_q, void* va_q,
+                  void* vb_q, long long ld_q, hipStream_t st);
+
 extern "C" int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
                                const void* vb, long long ld_vb, int B, int HW, int C, void* za,
                                void* zb, long long ld_z, float* lse_a, float* lse_b, void* ws,
@@ -387,6 +468,34 @@ extern "C" int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va
       ((uintptr_t)zb & 7))
     return CN_ERR_ALIGN;
   if (!ws || ((uintptr_t)ws & 255) || ws_bytes < cn_coatt_f8_workspace_bytes(B, HW)) return CN_ERR_SHAPE;
+  return f8_fwd(vat, ld_vat, va, ld_va, vb, ld_vb, B, HW, za, zb, ld_z, lse_a, lse_b, ws, false,
+                nullptr, nullptr, nullptr, 0, st);
+}
+
+extern "C" size_t cn_coatt_f8_train_workspace_bytes(int B, int HW) {
+  return cn_coatt_f8_workspace_bytes(B, HW) + (size_t)B * (hwq128(HW) / 32) * 8 + 256;
+}
+
+extern "C" int cn_coatt_f8_train_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                                     const void* vb, long long ld_vb, int B, int HW, int C, void* za,
+                                     void* zb, long long ld_z, float* lse_a, float* lse_b,
+                                     void* vat_q, void* va_q, void* vb_q, long long ld_q, void* ws,
+                                     size_t ws_bytes, hipStream_t st) {
+  if (B <= 0 || HW <= 0 || C != D || !za || !zb || !lse_a || !lse_b || !vat_q || !va_q || !vb_q)
+    return CN_ERR_SHAPE;
+  if (ld_vat % 8 || ld_va % 8 || ld_vb % 8 || ld_z % 4 || ld_q % 8 || ld_q < C) return CN_ERR_ALIGN;
+  if (((uintptr_t)vat & 15) || ((uintptr_t)va & 15) || ((uintptr_t)vb & 15) || ((uintptr_t)za & 7) ||
+      ((uintptr_t)zb & 7) || ((uintptr_t)vat_q & 15) || ((uintptr_t)va_q & 15) || ((uintptr_t)vb_q & 15))
+    return CN_ERR_ALIGN;
+  if (!ws || ((uintptr_t)ws & 255) || ws_bytes < cn_coatt_f8_train_workspace_bytes(B, HW)) return CN_ERR_SHAPE;
+  return f8_fwd(vat, ld_vat, va, ld_va, vb, ld_vb, B, HW, za, zb, ld_z, lse_a, lse_b, ws, true,
+                vat_q, va_q, vb_q, ld_q, st);
+}
+
+static int f8_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                  const void* vb, long long ld_vb, int B, int HW, void* za, void* zb, long long ld_z,
+                  float* lse_a, float* lse_b, void* ws, bool train, void* vat_q, void* va_q,
+                  void* vb_q, long long ld_q, hipStream_t st) {
   const int HWp = hwq128(HW), nt = hwp64(HW) / KT;
   const size_t rows = (size_t)B * HWp;
   unsigned char* p = (unsigned char*)ws;
@@ -401,15 +510,28 @@ extern "C" int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va
   unsigned char* vtas = p;
   const long long nr = (long long)rows * 8;
   const dim3 gr((unsigned)((nr + 255) / 256));
-  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vat, ld_vat, B, HW, HWp, a8, as);
+  unsigned char* bexp = nullptr;
+  if (train) {   // Vb's shared 32 x 32 block exponents (after the V^T scales, 256-aligned)
+    p = vtas + (size_t)B * nt * 512;
+    bexp = (unsigned char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    const long long nw = (long long)B * (HWp / 32) * 8;
+    hipLaunchKernelGGL(coatt_f8_blkexp_k, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st,
+                       (const bf16*)vb, ld_vb, B, HW, HWp / 32, bexp);
+    CN_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vat, ld_vat, B, HW, HWp, a8, as,
+                     (const unsigned char*)nullptr, (bf16*)vat_q, ld_q);
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, HWp, b8, bs);
+  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, HWp, b8, bs,
+                     (const unsigned char*)bexp, (bf16*)vb_q, ld_q);
   CN_CHECK_LAUNCH();
   const long long nv = (long long)B * nt * 2 * D;
   const dim3 gv((unsigned)((nv + 255) / 256));
-  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, nt, vtb, vtbs);
+  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, nt, vtb, vtbs,
+                     (const unsigned char*)bexp, HWp / 32, (bf16*)nullptr, 0ll);
   CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)va, ld_va, B, HW, nt, vta, vtas);
+  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)va, ld_va, B, HW, nt, vta, vtas,
+                     (const unsigned char*)nullptr, 0, (bf16*)va_q, ld_q);
   CN_CHECK_LAUNCH();
   F8Args a = {};
   // direction 0: Z_a = softmax_j(S) Vb  (queries Va_t, keys Vb, values Vb)

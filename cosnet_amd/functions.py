@@ -164,13 +164,18 @@ class CoattFn(F):
                 else:
                     ops.coatt_fused(vat, va, vb, n, hw, za, zb)                  # :160-170
                 return za, zb
-            # training: keep the per-row normalisers; the backward recomputes P from them.  The
-            # training forward is the bf16 flash kernel in fp8 mode too, so the backward's
-            # recomputed S and P are exactly the ones the forward normalised (the MX-fp8
-            # affinity serves the no-grad path above)
+            # training: keep the per-row normalisers; the backward recomputes P from them.  fp8
+            # mode (configs[4]): the MX-fp8 forward, which also hands back its operands DECODED
+            # (bf16, exact); the flash backward recomputes S and P from those and this forward's
+            # normalisers, so the gradient is the gradient of the fp8 forward (straight-through
+            # for the quantisations)
             lse_a = torch.empty((n, ops.hw_pad(hw)), dtype=torch.float32, device=dev)
             lse_b = torch.empty_like(lse_a)
-            ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)       # :160-170
+            ctx.q = None
+            if fp8:
+                ctx.q = ops.coatt_f8_train(vat, va, vb, n, hw, za, zb, lse_a, lse_b)  # :160-170
+            else:
+                ops.coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b)   # :160-170
             ctx.s = (va, vb, wf, vat, za, zb, lse_a, lse_b)
             ctx.flash = True
             ctx.link = link
@@ -263,7 +268,9 @@ class CoattFn(F):
           dVa_t = sum_j dS[i][j] Vb[j]                (cn_coatt_flash_dvat)
           dV_a  = [link] + sum_j P1[i][j] dZb[j]       (cn_coatt_flash_pv, S_row . dZ_b)
                   + dVa_t W                           (GEMM, the linear's input gradient)
-          dW    = dVa_t^T V_a                         (GEMM, the linear's weight gradient)"""
+          dW    = dVa_t^T V_a                         (GEMM, the linear's weight gradient)
+        fp8 mode: S, P and dS from the decoded MX operands of the fp8 forward; the linear's
+        GEMMs (bf16 in both modes) use the real V_a."""
         va, vb, wf, vat, za, zb, lse_a, lse_b = ctx.s
         n, hw, c, _ = ctx.geo
         dt = va.dtype
@@ -282,7 +289,10 @@ class CoattFn(F):
             if dv_link is not None:
                 ops.cast_copy(dv_link, dva)
                 mode = 2
-        dvat = ops.coatt_flash_bwd(vat, va, vb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw,
+        # the operands the forward's products read: the decoded MX-fp8 ones in fp8 mode
+        qvat, qva, qvb = ctx.q if ctx.q is not None else (vat, va, vb)
+        ctx.q = None
+        dvat = ops.coatt_flash_bwd(qvat, qva, qvb, wf, za, zb, lse_a, lse_b, dza, dzb, n, hw,
                                    dva=dva, dva_accumulate=mode == 2)
         if need_va:
             if dzb is not None:

@@ -543,6 +543,23 @@ def coatt_f8(vat, va, vb, n, hw, za, zb, lse_a=None, lse_b=None):
     return za, zb
 
 
+def coatt_f8_train(vat, va, vb, n, hw, za, zb, lse_a, lse_b):
+    """Training forward of both directions with MX-fp8 operands (configs[4]): Z_a, Z_b, the
+    per-row log2-sum-exp2 normalisers, and the decoded operands (vat_q, va_q, vb_q) -- bf16,
+    exact -- that the flash backward recomputes S and P from (cn_coatt_f8_train_fwd)."""
+    c = vat.shape[1]
+    ev = _prof_start(3 * 2.0 * n * hw * hw * c, ("coatt_f8_train_fwd", n, hw, c),
+                     (3 * n * hw * c + 2 * n * hw * c) * vat.element_size())
+    nws = int(nv.query("cn_coatt_f8_train_workspace_bytes", n, hw))
+    ws = torch.empty((nws,), dtype=torch.uint8, device=vat.device)
+    q = [torch.empty((n * hw, c), dtype=torch.bfloat16, device=vat.device) for _ in range(3)]
+    nv.call("cn_coatt_f8_train_fwd", vat.data_ptr(), ld(vat), va.data_ptr(), ld(va), vb.data_ptr(),
+            ld(vb), n, hw, c, za.data_ptr(), zb.data_ptr(), ld(za), lse_a.data_ptr(), lse_b.data_ptr(),
+            q[0].data_ptr(), q[1].data_ptr(), q[2].data_ptr(), c, ws.data_ptr(), nws, nv.stream())
+    _prof_end(ev)
+    return tuple(q)
+
+
 def coatt_flash_fwd(vat, va, vb, n, hw, za, zb, lse_a, lse_b):
     """Training forward of both co-attention directions (S never in HBM) + the per-row
     log2-sum-exp2 normalisers [n, hw_pad(hw)] the backward recomputes P from."""

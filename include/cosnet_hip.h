@@ -262,6 +262,20 @@ int cn_coatt_f8_fwd(const void* vat, long long ld_vat, const void* va, long long
                     const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                     long long ld_z, float* lse_a, float* lse_b, void* ws, size_t ws_bytes,
                     hipStream_t stream);
+/* fp8 co-attention forward for TRAINING (configs[4] "fp8 MFMA affinity", the forward whose
+ * gradient cn_coatt_flash_dvat / cn_coatt_flash_pv then compute): cn_coatt_f8_fwd with lse_a /
+ * lse_b required, Vb quantised with one E8M0 exponent per 32 keys x 32 channels (so its row
+ * image -- the S operand -- and its V^T image -- the P V operand of Z_a -- decode to the same
+ * values), and the DECODED MX operands written as bf16 (exact): vat_q (Va_t rows), va_q (Va as the
+ * V of Z_b), vb_q (Vb, every role); [B*HW][ld_q], 16-byte aligned.  The flash backward run on
+ * (vat_q, va_q, vb_q) and this forward's lse is the gradient of this forward (straight-through
+ * for the operand and P quantisations).  ws: cn_coatt_f8_train_workspace_bytes(B, HW) bytes,
+ * 256-byte aligned.  Reference: rgbd_segmentation_RAA.py:160-170, :213-221. */
+size_t cn_coatt_f8_train_workspace_bytes(int B, int HW);
+int cn_coatt_f8_train_fwd(const void* vat, long long ld_vat, const void* va, long long ld_va,
+                          const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
+                          long long ld_z, float* lse_a, float* lse_b, void* vat_q, void* va_q,
+                          void* vb_q, long long ld_q, void* ws, size_t ws_bytes, hipStream_t stream);
 int cn_coatt_fused_fwd_ws(const void* vat, long long ld_vat, const void* va, long long ld_va,
                           const void* vb, long long ld_vb, int B, int HW, int C, void* za, void* zb,
                           long long ld_z, void* ws, size_t ws_bytes, hipStream_t stream);

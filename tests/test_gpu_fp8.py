@@ -1,17 +1,22 @@
 """fp8 (OCP e4m3 / e5m2) path, BASELINE configs[4]: statistical parity with bf16.
 
-The fp8 path changes the forward conv GEMM operands (e4m3), the dgrad operands of the
-compute-heavy convs (e5m2 output gradients x e4m3 transposed weights) and -- for the no-grad
-co-attention -- the affinity / gather operands (cosnet_amd/fp8.py); the training co-attention
-stays the bf16 flash pair, so its gradient is the gradient of its forward.  Parity is
-statistical, with the bounds DESIGN §3.5 states: over 4 seeded SGD steps
-at 97x97 (B = 2 pairs), each on a different seeded batch, the mean fp8 loss within 5 % of the
-mean bf16 loss, every step within 15 %, the step-0 gap (same weights: the forward's precision
-alone) within 8 %, and the output maps' means within 0.03.  The distribution these bounds are
-set against, 5 seeds x {fp32, bf16, fp8} (tools/fp8_curve_dist.py, profiles/r04_fp8_curve_dist.json):
-mean gap 1.0-4.0 % (median 1.8 %), per-step gap median 4.1 %, p90 7.9 %, max 14.7 %, map-mean gap
-<= 0.026 -- while bf16 itself is up to 18 % per step and 0.032 in map mean away from fp32 on the
-same batches (this random-init 101-layer net is chaotic in low precision).  The kernels
+The fp8 path changes the forward conv GEMM operands (e4m3), the dgrad and 3x3 weight-gradient
+operands of the compute-heavy convs (e5m2 output gradients x e4m3), and the co-attention's
+affinity / gather operands (MX-fp8) in inference AND training -- the training backward
+recomputes S and P from the fp8 forward's decoded operands and normalisers, so its gradient is
+the gradient of its forward (tests/test_gpu_coatt_f8.py).  Parity is statistical (SURVEY.md §7
+step 9), with the bounds DESIGN §3.5 states: over 4 seeded SGD steps at 97x97 (B = 2 pairs),
+each on a different seeded batch, the mean fp8 loss within 5 % of the mean bf16 loss, every step
+within 15 %, the step-0 gap (same weights: the forward's precision alone) within 8 %, and the
+output maps' means within 0.045.  The distribution these bounds are set against, 8 seeds x
+{fp32, bf16, fp8} of the round-6 path (tools/fp8_curve_dist.py, profiles/r06_fp8_curve_dist.json):
+mean gap 0.4-3.7 % (median 1.0 %), per-step gap median 2.6 %, p90 6.0 %, max 7.7 % (round 4,
+bf16 training co-attention: 4.1 / 7.9 / 14.7 %), map-mean gap <= 0.035 (round 4: 0.026) --
+while bf16 itself is up to 7.9 % per step and 0.040 in map mean away from fp32 on the same
+batches (this random-init 101-layer net is chaotic in low precision).  The map bound is the
+bf16 path's own distance from fp32 on that distribution (0.040) plus 0.005: the fp8 affinity
+moves the attention weights by ~e^(+-1) (logits of std ~16, 3 mantissa bits per operand), so
+the trained maps sit further from bf16 than with the bf16 training co-attention of round 4.  The kernels
 themselves are pinned exactly in test_gpu_kernels.py (test_fp8_quant_matches_torch_e4m3fn,
 test_conv_fwd_fp8).
 """
@@ -58,10 +63,11 @@ def test_fp8_training_loss_curve_tracks_bf16(cuda):
     l8, m8, model = _run(cuda, True, False)
     assert np.isfinite(l8).all()
     rel = np.abs(l8 - l16) / np.abs(l16)
-    # this seed (100) in the committed distribution: step gaps 4.3 / 7.5 / 6.7 / 3.6 %, mean 1.3 %
+    # this seed (100) in the committed distribution: step gaps 4.4 / 2.7 / 5.1 / 4.1 %, mean 1.0 %
     assert rel[0] <= 0.08, (l8, l16)     # same weights: the forward's precision alone
     assert abs(l8.mean() - l16.mean()) <= 0.05 * l16.mean() and (rel <= 0.15).all(), (l8, l16)
-    assert abs(m8[0] - m16[0]) <= 0.03 and abs(m8[1] - m16[1]) <= 0.03, (m8, m16)
+    # this seed in profiles/r06_fp8_curve_dist.json: 0.035 / 0.011
+    assert abs(m8[0] - m16[0]) <= 0.045 and abs(m8[1] - m16[1]) <= 0.045, (m8, m16)
     ctx = model.fp8
     assert len(ctx.weights._c) > 100 and len(ctx.acts.slots) > 50   # the encoders ran fp8
     assert len(ctx.grads.slots) >= 20                                # and their dgrads (e5m2)

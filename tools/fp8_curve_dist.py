@@ -4,8 +4,8 @@ several seeds: the distribution tests/test_gpu_fp8.py's bounds are set from.
     python tools/fp8_curve_dist.py [nseeds] [out.json]
 
 For each seed base s: the same name-keyed weights, 4 SGD steps on the seeded batches s, s+1, ...
-(97x97, B = 2 pairs, the eager step), in fp32, bf16 and fp8 (e4m3 forward convs, e5m2 dgrads,
-MX-fp8 no-grad co-attention; bf16 training co-attention).  Prints per-step relative loss gaps
+(97x97, B = 2 pairs, the eager step), in fp32, bf16 and fp8 (e4m3 forward convs, e5m2 dgrads and
+3x3 weight gradients, MX-fp8 co-attention in inference and training since round 6).  Prints per-step relative loss gaps
 fp8 vs bf16, fp8 vs fp32 and bf16 vs fp32 (the bf16 path's own floor on this chaotic
 random-init network) and writes them as JSON.
 """
