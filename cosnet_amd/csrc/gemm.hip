@@ -502,6 +502,71 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid, kbeg);
   lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid, kbeg);
 
+  // Epilogue geometry (below) and the epilogue operands that do not depend on the product,
+  // loaded BEFORE the K loop so their latency hides behind it (the pass loop then prefetches
+  // pass p + 1's rows during pass p): EPI 2 (BN-backward reduce) -- the per-column affine of the
+  // forward apply and the pre-BN input rows; EPI 3 (read-add-store, c_mode 2: dgrad accumulating
+  // into the residual gradient) -- the old C rows.  Loaded at the epilogue (round 5 and before),
+  // their HBM latency sat exposed at the end of every block (~8-10 us per launch in the step).
+  constexpr int LDC = BN + 4;
+  constexpr int HR = (BM * LDC * 4 <= S * STAGE) ? BM
+                   : ((BM / 2) * LDC * 4 <= S * STAGE) ? BM / 2
+                   : ((BM / 4) * LDC * 4 <= S * STAGE) ? BM / 4 : BM / 8;
+  static_assert(HR % 16 == 0 && HR * LDC * 4 <= S * STAGE, "epilogue staging must fit in the LDS image");
+  static_assert(!KSG || HR == BM, "KSG sums the two groups' tiles in one staging pass");
+  constexpr int GPR = BN / 8;            // 8-column groups per row
+  constexpr int RPP = NT / GPR;          // rows per pass
+  constexpr int IT = HR / RPP;           // rows per thread per pass
+  static_assert(IT * RPP == HR, "epilogue rows per pass must be a multiple of the row stride");
+  constexpr int smode = EPI == 3 ? 0 : EPI;   // BN epilogue (compile-time: its registers would
+                                              // otherwise cost every plain GEMM occupancy)
+  constexpr bool PFC = EPI == 3;
+  constexpr int PQ = (int)sizeof(CT) / 2;     // 16-B chunks per 8 elements of C
+  static_assert(!PFC || sizeof(CT) == 2, "EPI 3: bf16 C");
+  const int c0t = (tid % GPR) * 8;            // this thread's columns within the tile (fixed)
+  CT* Cb = (p.ngroup ? (CT*)p.grp.C[batch] : (CT*)p.C + (long long)batch * p.c_bs) +
+           (p.c_mode == 3 ? (long long)split * p.slab : 0);
+  u32x4 xnx[(smode == 2 || PFC) ? IT * PQ : 1];   // the next staging pass's rows
+  auto epi_fetch = [&](int pass) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int row = m0 + pass * HR + tid / GPR + it * RPP;
+      const int col = n0 + c0t;
+      if constexpr (smode == 2) {
+        const bool ok = row < p.M && col + 8 <= p.N;
+        const u32x4* src = (const u32x4*)((const CT*)p.br_x + (long long)(ok ? row : m0) * p.br_ldx + (ok ? col : 0));
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) xnx[it * PQ + q] = src[q];
+      } else if constexpr (PFC) {
+        const CT* dst = Cb + (long long)row * p.ldc + col;
+        const bool ok = row < p.M && col + 8 <= p.N && ((uintptr_t)dst % 16 == 0);
+        xnx[it] = ok ? *(const u32x4*)dst : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  // EARLY: the prefetch registers stay live across the K loop -- only where that costs no spill
+  // (tiles without the 128-VGPR occupancy bound of the 2-stage BN-epilogue kernels and below
+  // 256 x 256, whose accumulators fill the register file; tools/kernel_resources.py checks)
+  constexpr bool EARLY = PFC || (smode == 2 && S >= 3 && BM * BN <= 128 * 128);
+  float bk1[8], bsf[8], bmu[8];
+  auto epi_affine = [&]() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = n0 + c0t + e;
+      const bool in = c < p.N;
+      const float g = in ? (p.br_gamma ? p.br_gamma[c] : 1.f) : 0.f;
+      const float b = in ? (p.br_beta ? p.br_beta[c] : 0.f) : 0.f;
+      const float is = in ? p.br_invstd[c] : 0.f;
+      bmu[e] = in ? p.br_mean[c] : 0.f;
+      bk1[e] = g * is;                  // the forward apply's affine (bn.hip bn_apply_k): the
+      bsf[e] = b - bmu[e] * bk1[e];     // recomputed ReLU mask has exactly the forward's sign
+    }
+  };
+  if constexpr (EARLY) {
+    if constexpr (smode == 2) epi_affine();
+    epi_fetch(0);
+  }
+
   f32x4 acc[RM][RN];
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -725,12 +790,6 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   // contiguous atomics).  Lane holds C[4g + r][l & 15] of each 16x16 block.
   // BN epilogues (st_mode, gemm.h) accumulate per-column partials of the stored values in the
   // same loop (registers), reduced over the block in a fixed order at the end.
-  constexpr int LDC = BN + 4;
-  constexpr int HR = (BM * LDC * 4 <= S * STAGE) ? BM
-                   : ((BM / 2) * LDC * 4 <= S * STAGE) ? BM / 2
-                   : ((BM / 4) * LDC * 4 <= S * STAGE) ? BM / 4 : BM / 8;
-  static_assert(HR % 16 == 0 && HR * LDC * 4 <= S * STAGE, "epilogue staging must fit in the LDS image");
-  static_assert(!KSG || HR == BM, "KSG sums the two groups' tiles in one staging pass");
   float* cs = (float*)smem;
   float alpha = p.alpha;
   {
@@ -740,52 +799,27 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
     if (sa) alpha *= *sa;
     if (sb) alpha *= *sb;
   }
-  CT* Cb = (p.ngroup ? (CT*)p.grp.C[batch] : (CT*)p.C + (long long)batch * p.c_bs) +
-           (p.c_mode == 3 ? (long long)split * p.slab : 0);
   const int cmode = p.c_mode == 3 ? 0 : p.c_mode;
-  constexpr int GPR = BN / 8;            // 8-column groups per row
-  constexpr int RPP = NT / GPR;          // rows per pass
-  constexpr int smode = EPI;             // BN epilogue (compile-time: its registers would
-                                         // otherwise cost every plain GEMM occupancy)
-  const int c0t = (tid % GPR) * 8;       // this thread's columns within the tile (fixed)
   float sk[8], sa1[8], sa2[8], sb1[8], sb2[8];
-  float bk1[8], bsf[8], bmu[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sk[e] = 0.f; sa1[e] = sa2[e] = sb1[e] = sb2[e] = 0.f; }
   int segA_end = 0x7fffffff;
-  if constexpr (smode == 1) {
-    segA_end = (m0 / p.st_seg_rows + 1) * p.st_seg_rows;
-  } else if constexpr (smode == 2) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = n0 + c0t + e;
-      const bool in = c < p.N;
-      const float g = in ? (p.br_gamma ? p.br_gamma[c] : 1.f) : 0.f;
-      const float b = in ? (p.br_beta ? p.br_beta[c] : 0.f) : 0.f;
-      const float is = in ? p.br_invstd[c] : 0.f;
-      bmu[e] = in ? p.br_mean[c] : 0.f;
-      bk1[e] = g * is;                  // the forward apply's affine (bn.hip bn_apply_k): the
-      bsf[e] = b - bmu[e] * bk1[e];     // recomputed ReLU mask has exactly the forward's sign
-    }
-  }
-  constexpr int IT = HR / RPP;          // rows per thread per pass
-  static_assert(IT * RPP == HR, "epilogue rows per pass must be a multiple of the row stride");
+  if constexpr (smode == 1) segA_end = (m0 / p.st_seg_rows + 1) * p.st_seg_rows;
+  if constexpr (smode == 2 && !EARLY) epi_affine();
 #pragma unroll 1
   for (int pass = 0; pass < BM / HR; ++pass) {
-    u32x4 xpf[smode == 2 ? IT * (int)sizeof(CT) / 2 : 1];
-    if constexpr (smode == 2) {
-      // BN-backward epilogue: issue this pass's loads of the pre-BN input first, so they are in
-      // flight while the accumulators are staged through LDS
+    // EARLY: this pass's rows were prefetched (before the K loop / during the previous pass) and
+    // the next pass's loads go out now.  Otherwise this pass's loads go out now, in flight while
+    // the accumulators are staged through LDS.
+    u32x4 xpf[(smode == 2 || PFC) ? IT * PQ : 1];
+    if constexpr (EARLY) {
 #pragma unroll
-      for (int it = 0; it < IT; ++it) {
-        const int row = m0 + pass * HR + tid / GPR + it * RPP;
-        const int col = n0 + c0t;
-        constexpr int Q = (int)sizeof(CT) / 2;  // 16-B chunks per 8 elements
-        const bool ok = row < p.M && col + 8 <= p.N;
-        const u32x4* src = (const u32x4*)((const CT*)p.br_x + (long long)(ok ? row : m0) * p.br_ldx + (ok ? col : 0));
+      for (int i = 0; i < IT * PQ; ++i) xpf[i] = xnx[i];
+      if (pass + 1 < BM / HR) epi_fetch(pass + 1);
+    } else if constexpr (smode == 2) {
+      epi_fetch(pass);
 #pragma unroll
-        for (int q = 0; q < Q; ++q) xpf[it * Q + q] = src[q];
-      }
+      for (int i = 0; i < IT * PQ; ++i) xpf[i] = xnx[i];
     }
     {
       const int g = lane >> 4;
@@ -850,7 +884,8 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
         if constexpr (sizeof(CT) == 2) {
           if (cmode == 2) {
             float q[8];
-            Chunk<bf16>::unpack(*(const u32x4*)dst, q);
+            if constexpr (PFC) Chunk<bf16>::unpack(xpf[it], q);   // prefetched (same condition)
+            else Chunk<bf16>::unpack(*(const u32x4*)dst, q);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += q[e];
           }
@@ -1078,8 +1113,29 @@ static int launch_epi(const GemmArgs& a, hipStream_t st) {
   }
 }
 
+// Read-add-store launches (c_mode 2, bf16 C: a dgrad accumulating into the residual gradient)
+// take the EPI 3 epilogue, whose old C rows are prefetched before the K loop.  CN_GEMM_PFC=0
+// keeps the plain epilogue (A/B runs).
+static bool pfc_on() {
+  static const bool on = [] { const char* e = getenv("CN_GEMM_PFC"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 template <class T, class CT, int LA, int LB>
 static int launch_tile(const GemmArgs& a, int batch, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && sizeof(CT) == 2 && (LA == L_KC_DENSE || LA == L_KC_CONV) &&
+                LB == L_KC_DENSE) {
+    if (a.c_mode == 2 && !a.row_map && !a.ngroup && pfc_on()) {
+      switch (pick_cfg(a, batch)) {
+        case 10: return launch_c<T, CT, 10, LA, LB, 3>(a, batch, st);
+        case 11: return launch_c<T, CT, 11, LA, LB, 3>(a, batch, st);
+        case 12: return launch_c<T, CT, 12, LA, LB, 3>(a, batch, st);
+        case 13: return launch_c<T, CT, 13, LA, LB, 3>(a, batch, st);
+        case 20: return launch_c<T, CT, 20, LA, LB, 3>(a, batch, st);
+        default: break;
+      }
+    }
+  }
   if constexpr (sizeof(T) == 4) {
     if (a.N <= 64 || cfg_blocks(1, a, batch) < 384) return launch_c<T, CT, 0, LA, LB>(a, batch, st);
     return launch_c<T, CT, 1, LA, LB>(a, batch, st);

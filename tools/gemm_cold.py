@@ -56,7 +56,7 @@ def gtime_sets(fns, reps=3):
 
 def main():
     flt = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] != "all" else ""
-    cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [-1, 11, 13, 14, 7, 2]
+    cfgs = [int(c) for a in sys.argv[2:] for c in a.split(",")] if len(sys.argv) > 2 else [-1, 11, 13, 14, 7, 2]
     for (name, op, n, cin, h, w, cout, k, p, d) in SHAPES:
         if flt not in name:
             continue
