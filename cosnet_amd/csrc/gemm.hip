@@ -490,9 +490,36 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   }
   const int m0 = tm * BM, n0 = tn * BN;
   const int batch = bz / p.nsplit, split = bz - batch * p.nsplit;
-  const int kbeg = split * p.k_chunk;
-  const int kend = min(p.K, kbeg + p.k_chunk);
-  const int nt = (kend - kbeg + BK - 1) / BK;
+  int kbeg = split * p.k_chunk;
+  int kend = min(p.K, kbeg + p.k_chunk);
+  if constexpr (LA == L_KC_CONV) {
+    // Vertical tap skipping (conv forward / stride-1 dgrad gathers; k = (r, s, ci), r-major): the
+    // taps r whose source rows y = oy st + off_y + r step_y miss the image for EVERY row of this
+    // tile contribute exact zeros, and the valid r form one interval, so the block runs only the
+    // K range of taps [r_lo, r_hi] -- e.g. the ASPP's dilation-12 / 18 convs on the 60 x 60 map,
+    // where a 256-row tile (~4 image rows) near the top or bottom edge has a whole tap row of
+    // padding.  Uniform per block (the tile's first / last row); a tile spanning two images
+    // keeps every tap.
+    const ConvGeom& g = p.ga;
+    if (g.KH > 1) {
+      int i0, i1, rm0, rm1, oy0, oy1, ox;
+      fdivmod(m0, g.div_OHW, i0, rm0);
+      fdivmod(min(m0 + BM, p.M) - 1, g.div_OHW, i1, rm1);
+      fdivmod(rm0, g.div_OW, oy0, ox);
+      fdivmod(rm1, g.div_OW, oy1, ox);
+      if (i0 != i1) { oy0 = 0; oy1 = g.OH - 1; }
+      const int ylo = oy0 * g.st + g.off_y, yhi = oy1 * g.st + g.off_y;
+      int rlo = g.KH, rhi = -1;
+      for (int r = 0; r < g.KH; ++r) {
+        const int a = ylo + r * g.step_y, b = yhi + r * g.step_y;
+        if (max(min(a, b), 0) <= min(max(a, b), g.H - 1)) { rlo = min(rlo, r); rhi = r; }
+      }
+      const int kt0 = rlo * g.KW * g.C, kt1 = (rhi + 1) * g.KW * g.C;
+      kbeg = max(kbeg, kt0);
+      kend = min(kend, kt1);
+    }
+  }
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   const T* Abase = p.ngroup ? (const T*)p.grp.A[batch] : (const T*)p.A + (long long)batch * p.a_bs;
   const T* Bbase = p.ngroup ? (const T*)p.grp.B[batch] : (const T*)p.B + (long long)batch * p.b_bs;

@@ -323,3 +323,37 @@ def test_q48_row_maximum_growth(cuda, n, hw):
         assert rel(got, ref) <= TOL, (k, rel(got, ref))
     for k in (4, 5):
         assert (v1[k] - v5[k]).abs().max().item() <= 1e-4 * max(1.0, v1[k].abs().max().item()), k
+
+
+@pytest.mark.parametrize("n,hw", [(4, 3600), (5, 3600)])
+def test_q48_pv_split_partials_under_cancellation(cuda, n, hw):
+    """The 48-row kernel's cut items store their un-normalised partial O rows in bf16 (round 5;
+    the 4-wave kernel kept fp32).  In the PV backward kernel (dV_a += sum_j P1[i][j] dZb[j]) the
+    gradient dZb has random signs, so segment partials can cancel and each partial's bf16 rounding
+    is relative to the partial, not to the (smaller) result.  Worst case here: nearly flat
+    softmaxes (features x 0.25: logit std ~1) and dZb = +-1 alternating over the keys, so each row
+    sums ~3600 terms that cancel to ~1/60 of their magnitude.  Pinned against fp64 per row,
+    relative to the row's magnitude scale sum_j P1[i][j] |dZb[j]| (the scale a partial's rounding
+    is relative to): <= 2^-8 for the split plan; the 4-wave kernel (fp32 partials, only the final
+    bf16 rounding) is measured beside it, and both errors relative to the row's own result are
+    printed."""
+    lib = nv.load()
+    vat, va, vb = make(n, hw, 256, cuda, seed=hw + 29, scale=0.25)
+    sgn = torch.where(torch.arange(n * hw) % 2 == 0, 1.0, -1.0)[:, None]
+    g = torch.Generator().manual_seed(n * hw + 6)
+    dzb = (sgn * (1.0 + 0.1 * torch.rand((n * hw, 256), generator=g))).to(torch.bfloat16).to(cuda)
+    c = 256
+    S = vat.double().reshape(n, hw, c) @ vb.double().reshape(n, hw, c).transpose(1, 2)
+    P1 = torch.softmax(S, dim=1)                                   # over i for each key j
+    d = dzb.double().reshape(n, hw, c)
+    ref = (P1 @ d).reshape(n * hw, c)
+    scale = (P1 @ d.abs()).reshape(n * hw, c)
+    out = {}
+    for v in (5, 1):
+        pv = _run_variant(lib, v, vat, va, vb, dzb, n, hw, cuda)[6]
+        err = (pv.double() - ref).abs()
+        out[v] = ((err / scale).max().item(), (err.norm() / ref.norm()).item())
+    print("PV under cancellation n=%d hw=%d: |ref|/scale %.3f; q48 (bf16 partials) max err/scale "
+          "%.2e, rel L2 %.2e; 4-wave (fp32 partials) %.2e, %.2e" % (
+              n, hw, (ref.abs() / scale).mean().item(), out[5][0], out[5][1], out[1][0], out[1][1]))
+    assert out[5][0] <= 2 ** -8, out
