@@ -1249,8 +1249,15 @@ static int launch_kinds(const GemmArgs& a, int la, int lb, int batch, hipStream_
 // three tiles the shape heuristic uses; 128 fp8 per 128-byte K tile, one scaled MFMA per tile.
 template <class CT, int LA, class T8 = f8e4m3>
 static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
-  // (the 256x256 tile would spill its fp8 fragments: 128x128 serves the wide products too)
+  // (the 256x256 tile would spill its fp8 fragments: 128x128 serves the wide products too).
+  // Round 6: CN_GEMM_F8BIG = 8 (256x128) or 9 (128x256), 8 waves of 64x64 -- a quarter fewer LDS
+  // fill bytes per FLOP than 128x128 -- for the products with >= 256 such tiles (A/B runs).
+  static const int big = [] { const char* e = getenv("CN_GEMM_F8BIG"); return e ? atoi(e) : 0; }();
   const int c = pick_cfg(a, batch);
+  if ((big == 8 || big == 9) && c != 12 && tiles_of(big, a.M, a.N) * batch >= 256) {
+    if (big == 8) return launch_c<T8, CT, 8, LA, L_KC_DENSE>(a, batch, st);
+    return launch_c<T8, CT, 9, LA, L_KC_DENSE>(a, batch, st);
+  }
   if (c == 12) return launch_c<T8, CT, 12, LA, L_KC_DENSE>(a, batch, st);
   if (c == 13) return launch_c<T8, CT, 13, LA, L_KC_DENSE>(a, batch, st);
   return launch_c<T8, CT, 11, LA, L_KC_DENSE>(a, batch, st);
