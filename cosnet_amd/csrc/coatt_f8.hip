@@ -226,6 +226,132 @@ __global__ __launch_bounds__(256) void coatt_f8_vt_k(const bf16* __restrict__ v,
   vts[bt * 512 + u * 256 + (d & 31) * 8 + (d >> 5)] = (unsigned char)e;
 }
 
+// ---- training prepass, one launch for the three operands (round 6) -----------------------------
+// Block = (32-key block kb of batch entry b, operand): the 32 x 256 tile is loaded once (thread =
+// (row, 32-channel block), 64 bytes), staged in LDS for the column (per-channel) statistics, and
+// every MX image the forward reads plus the decoded bf16 copy the backward reads is written from
+// it:  op 0 = Va_t: row image, exponents per (row, 32 channels);  op 1 = Vb: row image AND V^T
+// image with one exponent per 32 keys x 32 channels;  op 2 = Va: V^T image, exponents per
+// (channel, 32 keys).  Same bytes as coatt_f8_rows_k / coatt_f8_vt_k / coatt_f8_blkexp_k (five
+// launches, ~84 us at 8 pairs) produce.
+struct F8Prep {
+  const bf16* x[3]; long long ldx[3];
+  unsigned char* x8[2]; unsigned char* xs[2];        // row images of op 0, op 1
+  unsigned char* vt8[2]; unsigned char* vts[2];      // V^T images of op 1, op 2
+  bf16* dq[3]; long long lddq;
+  int B, HW, HWp, nt;
+};
+
+__global__ __launch_bounds__(256) void coatt_f8_prep_k(F8Prep a) {
+  __shared__ bf16 tile[32][D];
+  __shared__ float red[4][8];
+  __shared__ int bex[8];
+  const int op = blockIdx.y;
+  const int nkb = a.HWp >> 5;
+  const int kb = blockIdx.x % nkb, b = blockIdx.x / nkb;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = tid >> 3, c = tid & 7;                 // this thread's row and 32-channel block
+  const int key = kb * 32 + r;
+  float v[32];
+  if (key < a.HW) {
+    const bf16* src = a.x[op] + ((long long)b * a.HW + key) * a.ldx[op] + 32 * c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x4 u = *(const u32x4*)(src + 8 * q);
+      *(u32x4*)&tile[r][32 * c + 8 * q] = u;
+      Chunk<bf16>::unpack(u, v + 8 * q);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(u32x4*)&tile[r][32 * c + 8 * q] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = 0.f;
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  if (op == 1) {   // the 32 x 32 block's maximum: lanes of one channel block, then the 4 waves
+    float m = amax;
+    m = fmaxf(m, __shfl_xor(m, 8, 64));
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    if (lane < 8) red[w][lane] = m;
+  }
+  __syncthreads();
+  if (op == 1 && tid < 8)
+    bex[tid] = e8m0_of(fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid])));
+  __syncthreads();
+  const long long prow = (long long)b * a.HWp + key;
+  if (op < 2) {   // row image (+ its decoded copy)
+    const int e = op == 1 ? bex[c] : e8m0_of(amax);
+    const float inv = ldexpf(1.f, 127 - e);
+    unsigned wd[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      wd[i] = pk4(clampf8(v[4 * i] * inv), clampf8(v[4 * i + 1] * inv), clampf8(v[4 * i + 2] * inv),
+                  clampf8(v[4 * i + 3] * inv));
+    unsigned char* dst = a.x8[op] + prow * D + 32 * c;
+    *(u32x4*)dst = u32x4{wd[0], wd[1], wd[2], wd[3]};
+    *(u32x4*)(dst + 16) = u32x4{wd[4], wd[5], wd[6], wd[7]};
+    a.xs[op][prow * 8 + 4 * (c & 1) + (c >> 1)] = (unsigned char)e;
+    if (key < a.HW) {
+      const float sc = ldexpf(1.f, e - 127);
+      bf16* dd = a.dq[op] + ((long long)b * a.HW + key) * a.lddq + 32 * c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = dec8(wd[2 * q + (j >> 2)], j & 3) * sc;
+        *(u32x4*)(dd + 8 * q) = Chunk<bf16>::pack(f);
+      }
+    }
+  }
+  if (op >= 1 && kb < 2 * a.nt) {   // V^T image: thread = channel d, the block's 32 keys
+    const int d = tid, u = kb & 1, t = kb >> 1;
+    float x[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) x[kk] = (float)tile[kk][d];
+    int e;
+    if (op == 1) {
+      e = bex[d >> 5];
+    } else {
+      float am = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) am = fmaxf(am, fabsf(x[kk]));
+      e = e8m0_of(am);
+    }
+    const float inv = ldexpf(1.f, 127 - e), sc = ldexpf(1.f, e - 127);
+    const long long bt = (long long)b * a.nt + t;
+    unsigned char* vt8 = a.vt8[op - 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float y[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) y[i] = clampf8(x[(i & 3) + 8 * (i >> 2) + 4 * h] * inv);
+      const u32x4 pw = u32x4{pk4(y[0], y[1], y[2], y[3]), pk4(y[4], y[5], y[6], y[7]),
+                             pk4(y[8], y[9], y[10], y[11]), pk4(y[12], y[13], y[14], y[15])};
+      *(u32x4*)(vt8 + (bt * D + d) * KT + 32 * h + 16 * u) = pw;
+      if (op == 2) {   // Va's decoded copy: into the LDS tile, stored row-wise below
+        const unsigned wd[4] = {pw.x, pw.y, pw.z, pw.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[(i & 3) + 8 * (i >> 2) + 4 * h] = dec8(wd[i >> 2], i & 3) * sc;
+      }
+    }
+    a.vts[op - 1][bt * 512 + u * 256 + (d & 31) * 8 + (d >> 5)] = (unsigned char)e;
+    if (op == 2) {
+      __syncthreads();   // every column read of the raw tile done
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) tile[kk][d] = (bf16)x[kk];
+      __syncthreads();
+      if (key < a.HW) {
+        bf16* dd = a.dq[2] + ((long long)b * a.HW + key) * a.lddq + 32 * c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(u32x4*)(dd + 8 * q) = *(const u32x4*)&tile[r][32 * c + 8 * q];
+      }
+    }
+  }
+}
+
 struct F8Dir {
   const unsigned char* q8; const unsigned char* qs;    // [B][HWp][256], [B][HWp][8]
   const unsigned char* k8; const unsigned char* ks;
@@ -510,29 +636,42 @@ static int f8_fwd(const void* vat, long long ld_vat, const void* va, long long l
   unsigned char* vtas = p;
   const long long nr = (long long)rows * 8;
   const dim3 gr((unsigned)((nr + 255) / 256));
-  unsigned char* bexp = nullptr;
-  if (train) {   // Vb's shared 32 x 32 block exponents (after the V^T scales, 256-aligned)
-    p = vtas + (size_t)B * nt * 512;
-    bexp = (unsigned char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
-    const long long nw = (long long)B * (HWp / 32) * 8;
-    hipLaunchKernelGGL(coatt_f8_blkexp_k, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st,
-                       (const bf16*)vb, ld_vb, B, HW, HWp / 32, bexp);
+  static const bool prep5 = [] { const char* e = getenv("CN_F8_PREP5"); return e && e[0] == '1'; }();
+  if (train && !prep5) {   // one launch: all three operands' images and decoded copies
+    F8Prep pa = {};
+    pa.x[0] = (const bf16*)vat; pa.x[1] = (const bf16*)vb; pa.x[2] = (const bf16*)va;
+    pa.ldx[0] = ld_vat; pa.ldx[1] = ld_vb; pa.ldx[2] = ld_va;
+    pa.x8[0] = a8; pa.xs[0] = as; pa.x8[1] = b8; pa.xs[1] = bs;
+    pa.vt8[0] = vtb; pa.vts[0] = vtbs; pa.vt8[1] = vta; pa.vts[1] = vtas;
+    pa.dq[0] = (bf16*)vat_q; pa.dq[1] = (bf16*)vb_q; pa.dq[2] = (bf16*)va_q; pa.lddq = ld_q;
+    pa.B = B; pa.HW = HW; pa.HWp = HWp; pa.nt = nt;
+    hipLaunchKernelGGL(coatt_f8_prep_k, dim3((unsigned)(B * (HWp / 32)), 3), dim3(256), 0, st, pa);
+    CN_CHECK_LAUNCH();
+  } else {
+    unsigned char* bexp = nullptr;
+    if (train) {   // Vb's shared 32 x 32 block exponents (after the V^T scales, 256-aligned)
+      p = vtas + (size_t)B * nt * 512;
+      bexp = (unsigned char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+      const long long nw = (long long)B * (HWp / 32) * 8;
+      hipLaunchKernelGGL(coatt_f8_blkexp_k, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st,
+                         (const bf16*)vb, ld_vb, B, HW, HWp / 32, bexp);
+      CN_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vat, ld_vat, B, HW, HWp, a8, as,
+                       (const unsigned char*)nullptr, (bf16*)vat_q, ld_q);
+    CN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, HWp, b8, bs,
+                       (const unsigned char*)bexp, (bf16*)vb_q, ld_q);
+    CN_CHECK_LAUNCH();
+    const long long nv = (long long)B * nt * 2 * D;
+    const dim3 gv((unsigned)((nv + 255) / 256));
+    hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, nt, vtb, vtbs,
+                       (const unsigned char*)bexp, HWp / 32, (bf16*)nullptr, 0ll);
+    CN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)va, ld_va, B, HW, nt, vta, vtas,
+                       (const unsigned char*)nullptr, 0, (bf16*)va_q, ld_q);
     CN_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vat, ld_vat, B, HW, HWp, a8, as,
-                     (const unsigned char*)nullptr, (bf16*)vat_q, ld_q);
-  CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(coatt_f8_rows_k, gr, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, HWp, b8, bs,
-                     (const unsigned char*)bexp, (bf16*)vb_q, ld_q);
-  CN_CHECK_LAUNCH();
-  const long long nv = (long long)B * nt * 2 * D;
-  const dim3 gv((unsigned)((nv + 255) / 256));
-  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)vb, ld_vb, B, HW, nt, vtb, vtbs,
-                     (const unsigned char*)bexp, HWp / 32, (bf16*)nullptr, 0ll);
-  CN_CHECK_LAUNCH();
-  hipLaunchKernelGGL(coatt_f8_vt_k, gv, dim3(256), 0, st, (const bf16*)va, ld_va, B, HW, nt, vta, vtas,
-                     (const unsigned char*)nullptr, 0, (bf16*)va_q, ld_q);
-  CN_CHECK_LAUNCH();
   F8Args a = {};
   // direction 0: Z_a = softmax_j(S) Vb  (queries Va_t, keys Vb, values Vb)
   a.dir[0] = F8Dir{a8, as, b8, bs, vtb, vtbs, (bf16*)za, ld_z, lse_a};
