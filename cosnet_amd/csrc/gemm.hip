@@ -198,6 +198,11 @@ template <class T, int ROWS, int KIND, int NT> struct Loader {
       }
     } else if constexpr (KIND == L_KC_CONV) {
       const int tap = __builtin_amdgcn_readfirstlane(fdiv(k0, g.div_C));
+#ifdef CN_PROBE_A_ONCE
+      // TIMING PROBE ONLY (results are wrong): the A tile of tap 0 stands in for every tap -- the
+      // upper bound of an input-halo loader that fills A once per channel chunk instead of per tap
+      if (tap != 0) return;
+#endif
       if (tap != ctap) {   // new tap (uniform branch): the chunks' pixel offsets
         int r, ss;
         fdivmod(tap, g.div_KW, r, ss);

@@ -311,6 +311,41 @@ def test_configs1_473_b4_bf16_step_tracks_fp32(cuda):
     assert 0.8 <= np.median(ratio) <= 1.25 and inside >= 0.9, (np.median(ratio), inside)
 
 
+def test_configs1_473_b4_bf16_step_vs_reference(cuda):
+    """configs[1] in bf16 against the REFERENCE's own run (tests/golden/train_b4_473.npz, the
+    reference in fp64 at this very configuration), not against our fp32 path: the aggregates a
+    training step consumes, with the bounds of test_configs1_473_b4_bf16_step_tracks_fp32 --
+    |loss - loss_ref| <= 3 %, mean(x1), mean(x2) within 0.03, per-parameter gradient norms: median
+    ratio within [0.8, 1.25] and >= 90 % of the parameters within [0.5, 2].  (Element parity is
+    not the bar in bf16: the random-init 101-layer network is chaotic under bf16 rounding -- the
+    reference itself run in bf16 agrees with its fp64 masks on ~80 % of pixels; bf16 blocks are
+    pinned elementwise to fp64 in tests/test_gpu_blocks_bf16.py.)"""
+    from conftest import golden_meta
+    z = golden("train_b4_473.npz")
+    meta = golden_meta()["train_b4_473"]
+    inp = synthetic_inputs(4, 473, 473, seed=1234)
+    assert [zlib.crc32(t.numpy().tobytes()) for t in inp] == list(z["in_crc32"])
+    inp = [t.to(cuda) for t in inp]
+    m = make_model(cuda, torch.bfloat16).train()
+    x1, x2, loss = _step_once(m, inp)
+    loss.backward()
+    torch.cuda.synchronize()
+    lref = float(z["f64/loss"][0])
+    assert np.isfinite(loss.item()) and abs(loss.item() - lref) <= 0.03 * abs(lref), (loss.item(), lref)
+    for name, t in (("x1", x1), ("x2", x2)):
+        ref = float(z["f64/mean/" + name][0])
+        assert abs(t.double().mean().item() - ref) <= 0.03, (name, t.double().mean().item(), ref)
+    named = dict(m.named_parameters())
+    norms = np.array([named[k].grad.double().norm().item() for k in meta["grad_norm_keys"]])
+    ref = z["f64/grad_norm"]
+    nz = ref >= 1e-6 * np.median(ref)          # analytically zero norms excluded
+    ratio = norms[nz] / ref[nz]
+    inside = ((ratio >= 0.5) & (ratio <= 2.0)).mean()
+    print("bf16 vs reference fp64 at 473x473 B=4: loss %.5f / %.5f, grad-norm ratio median %.3f, "
+          "%.1f %% within [0.5, 2]" % (loss.item(), lref, np.median(ratio), 100 * inside))
+    assert 0.8 <= np.median(ratio) <= 1.25 and inside >= 0.9, (np.median(ratio), inside)
+
+
 def test_configs1_graphed_train_step_bf16(cuda):
     """configs[1] through the recorded HIP-graph step bench.py times: two replays after the
     eager warmup give finite losses and finite, changed parameters."""
