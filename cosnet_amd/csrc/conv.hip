@@ -256,6 +256,36 @@ extern "C" int cn_conv_fwd_bn(int dtype, const void* x, long long ldx, int N, in
                                run_var, momentum, eps, st);
 }
 
+// fp8 conv (cn_conv_fwd_fp8) with the BN statistics in its GEMM epilogue (cn_conv_fwd_bn's
+// reduction of the stored bf16 y), for configs[4]'s long-K narrow convs.  ws:
+// cn_conv_fwd_bn_workspace_floats(DT_FP8, M, Cout, K) floats.
+extern "C" int cn_conv_fwd_fp8_bn(const void* x8, long long ldx, int N, int H, int W, int Cin,
+                                  const void* w8, int Cout, int KH, int KW, int stride, int pad,
+                                  int dil, const float* bias, void* y, long long ldy, int OH, int OW,
+                                  const float* x_state, const float* w_state, int nseg, float* ws,
+                                  float* mean, float* invstd, float* run_mean, float* run_var,
+                                  float momentum, float eps, hipStream_t st) {
+  if (Cin % 16 || ldx % 16 || ((uintptr_t)x8 & 15) || ((uintptr_t)w8 & 15)) return CN_ERR_ALIGN;
+  GemmArgs a;
+  int la;
+  int rc = conv_fwd_args(DT_BF16, x8, ldx, N, H, W, Cin, w8, Cout, KH, KW, stride, pad, dil, bias, y,
+                         ldy, OH, OW, a, la);
+  if (rc) return rc;
+  if (nseg < 1 || a.M % nseg || !ws) return CN_ERR_SHAPE;
+  a.scale_a = x_state;
+  a.scale_b = w_state;
+  const int bm = cn_gemm_bm(DT_FP8, a.M, a.N, a.K, -1);
+  const long long mt = (a.M + bm - 1) / bm;
+  a.st_mode = 1;
+  a.st_ws = ws;
+  a.st_plane = mt * Cout;
+  a.st_seg_rows = a.M / nseg;
+  rc = cn_gemm_dispatch(a, DT_FP8, 0, la, L_KC_DENSE, 1, st);
+  if (rc) return rc;
+  return cn_bn_tile_stats_impl(ws, a.st_plane, (int)mt, bm, a.M, nseg, Cout, mean, invstd, run_mean,
+                               run_var, momentum, eps, st);
+}
+
 extern "C" size_t cn_conv_dgrad_bn_workspace_floats(int dtype, int M, int Cin, int K) {
   return (size_t)2 * mtiles_of(dtype, M, Cin, K) * Cin;
 }

@@ -1259,6 +1259,15 @@ static int launch_f8(const GemmArgs& a, int batch, hipStream_t st) {
   // fill bytes per FLOP than 128x128 -- for the products with >= 256 such tiles (A/B runs).
   static const int big = [] { const char* e = getenv("CN_GEMM_F8BIG"); return e ? atoi(e) : 0; }();
   const int c = pick_cfg(a, batch);
+  if constexpr (sizeof(CT) == 2 && std::is_same<T8, f8e4m3>::value) {
+    // fp8 conv forward with the BN-statistics epilogue (round 6; the bf16 path's EPI 1)
+    if (a.st_mode == 1) {
+      if (c == 12) return launch_c<T8, CT, 12, LA, L_KC_DENSE, 1>(a, batch, st);
+      if (c == 13) return launch_c<T8, CT, 13, LA, L_KC_DENSE, 1>(a, batch, st);
+      return launch_c<T8, CT, 11, LA, L_KC_DENSE, 1>(a, batch, st);
+    }
+  }
+  if (a.st_mode) return CN_ERR_UNSUPPORTED;
   if ((big == 8 || big == 9) && c != 12 && tiles_of(big, a.M, a.N) * batch >= 256) {
     if (big == 8) return launch_c<T8, CT, 8, LA, L_KC_DENSE>(a, batch, st);
     return launch_c<T8, CT, 9, LA, L_KC_DENSE>(a, batch, st);
@@ -1296,7 +1305,8 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
   if (la == L_KC_CONV && (a.ga.C % bk != 0 || !buf_ok(L_KC_CONV, a, true, esz))) la = L_KC_CONV_G;
   if (!buf_ok(la, a, true, esz) || !buf_ok(lb, a, false, esz)) return CN_ERR_SHAPE;
   if (dtype == DT_FP8) {
-    if (lb != L_KC_DENSE || a.st_mode || a.nsplit != 1) return CN_ERR_UNSUPPORTED;
+    if (lb != L_KC_DENSE || a.nsplit != 1) return CN_ERR_UNSUPPORTED;
+    if (a.st_mode && (a.st_mode != 1 || batch != 1 || a.row_map || a.c_mode || c_f32)) return CN_ERR_UNSUPPORTED;
     if (la == L_KC_DENSE) return c_f32 ? launch_f8<float, L_KC_DENSE>(a, batch, st) : launch_f8<bf16, L_KC_DENSE>(a, batch, st);
     if (la == L_KC_CONV) return c_f32 ? launch_f8<float, L_KC_CONV>(a, batch, st) : launch_f8<bf16, L_KC_CONV>(a, batch, st);
     if (la == L_KC_CONV_G) return c_f32 ? launch_f8<float, L_KC_CONV_G>(a, batch, st) : launch_f8<bf16, L_KC_CONV_G>(a, batch, st);

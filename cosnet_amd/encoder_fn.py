@@ -60,6 +60,9 @@ WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "512"))
 # fp8 mode (configs[4]): the 3x3 bottleneck and ASPP weight gradients on fp8 operands
 # (cn_conv_wgrad_fp8); CN_WGRAD_FP8=0 keeps them bf16 (A/B runs).
 WGRAD_FP8 = os.environ.get("CN_WGRAD_FP8", "1") != "0"
+# fp8 mode: the BN statistics of the long-K narrow fp8 convs (fuse_stats) from the fp8 GEMM's
+# epilogue (cn_conv_fwd_fp8_bn) instead of their own pass; CN_FP8_FUSE_STATS=0 for A/B runs.
+FP8_FUSE_STATS = os.environ.get("CN_FP8_FUSE_STATS", "1") != "0"
 # TIMING PROBE ONLY (results are wrong): CN_PROBE_SKIP_APPLY=1 / 2 / 3 drops the bn1 / bn2 / both
 # BN + ReLU apply passes of every bottleneck (the next conv reads the raw conv output) -- the
 # upper bound of what folding those applies into the consumer conv's operand path could save
@@ -188,9 +191,9 @@ def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=
     """conv -> raw output c and the BN statistics of c per segment.  Train mode: the statistics
     come out of the conv's GEMM epilogue where that is cheaper (ops.conv_fwd_bn, no pass over c),
     else a separate statistics pass; eval: running statistics.  fp8 mode (configs[4]): the
-    conv GEMM takes e4m3 operands (cosnet_amd/fp8.py), statistics by the separate pass; with a
-    list q8 the e4m3 input copy is appended to it as Fp8Acts.saved() (for the fp8 weight
-    gradient)."""
+    conv GEMM takes e4m3 operands (cosnet_amd/fp8.py), statistics from its epilogue by the same
+    rule (ops.conv_fwd_fp8_bn) or the separate pass; with a list q8 the e4m3 input copy is
+    appended to it as Fp8Acts.saved() (for the fp8 weight gradient)."""
     cin = wf.shape[1] // (k * k)
     ctx = fp8_of(bn)
     if weight is not None and ctx is not None and fp8_ok(x, cin) and x.shape[0] > 64:
@@ -198,6 +201,11 @@ def conv_bn(x, n, h, w, wf, cout, k, stride, pad, dil, bn, training, nseg, bias=
         if q8 is not None:
             q8.append(ctx.acts.saved(x8, xs))
         wf8, ws = ctx.weights.get(weight)
+        if training and FP8_FUSE_STATS and fuse_stats(cout, wf.shape[1]):
+            # the statistics from the fp8 GEMM's epilogue, as the bf16 path takes them (round 6)
+            c, oh, ow, st = ops.conv_fwd_fp8_bn(x8, n, h, w, wf8, cout, k, stride, pad, dil, xs, ws,
+                                                bn, nseg, bias=bias)
+            return c, oh, ow, SegStats(st, nseg, cout)
         c, oh, ow = ops.conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, xs, ws, bias=bias)
         return c, oh, ow, seg_stats(c, bn, training, nseg)
     if training and fuse_stats(cout, wf.shape[1]):

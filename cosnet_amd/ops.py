@@ -324,6 +324,34 @@ def conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, 
     return out, oh, ow
 
 
+def conv_fwd_fp8_bn(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, bn, nseg=1,
+                    bias=None):
+    """conv_fwd_fp8 + the BN batch statistics of its stored bf16 output from the GEMM epilogue
+    (cn_conv_fwd_fp8_bn), as conv_fwd_bn does for bf16.  Returns (y, oh, ow, (mean, invstd))."""
+    cin = wf8.shape[1] // (k * k)
+    oh, ow = out_hw(h, w, k, stride, pad, dil)
+    M = n * oh * ow
+    if M % nseg or M // nseg <= 1:
+        raise ValueError("Expected more than 1 value per channel when training, got input size "
+                         "torch.Size([%d, %d, 1, 1])" % (M // nseg, cout))
+    out = torch.empty((M, cout), dtype=torch.bfloat16, device=x8.device)
+    mean = torch.empty((nseg * cout,), dtype=torch.float32, device=x8.device)
+    invstd = torch.empty_like(mean)
+    nws = int(nv.query("cn_conv_fwd_bn_workspace_floats", 2, M, cout, k * k * cin))
+    ws = torch.empty((nws,), dtype=torch.float32, device=x8.device)
+    ev = _prof_start(2.0 * M * cout * k * k * cin, ("fwd8", M, cout, k * k * cin),
+                     n * h * w * cin + cout * k * k * cin + 2 * M * cout)
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    nv.call("cn_conv_fwd_fp8_bn", x8.data_ptr(), ld(x8), n, h, w, cin, wf8.data_ptr(), cout, k, k,
+            stride, pad, dil, nv.ptr(bias), out.data_ptr(), ld(out), oh, ow, x_state.data_ptr(),
+            w_state.data_ptr(), nseg, ws.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+            bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(mom), float(bn.eps),
+            nv.stream())
+    _prof_end(ev)
+    bn._cn_nbt = getattr(bn, "_cn_nbt", 0) + nseg
+    return out, oh, ow, (mean, invstd)
+
+
 def conv_dgrad(dy, n, oh, ow, wt, cin, k, stride, pad, dil, h, w, out=None, accumulate=False):
     cout = wt.shape[1] // (k * k)
     if out is None:

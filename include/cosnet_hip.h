@@ -143,6 +143,14 @@ int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin,
  * [nseg][Cout]; running stats updated segment after segment (momentum, eps as nn.BatchNorm2d).
  * ws: cn_conv_fwd_bn_workspace_floats(dtype, M, Cout, KH*KW*Cin) floats. */
 size_t cn_conv_fwd_bn_workspace_floats(int dtype, int M, int Cout, int K);
+/* cn_conv_fwd_fp8 with the same BN-statistics epilogue (configs[4]: the fp8 forward convs whose
+ * statistics the bf16 path also takes from the epilogue); ws: cn_conv_fwd_bn_workspace_floats(
+ * 2 (fp8), M, Cout, K) floats.  Replaces nn.Conv2d + nn.BatchNorm2d's batch statistics as above. */
+int cn_conv_fwd_fp8_bn(const void* x8, long long ldx, int N, int H, int W, int Cin, const void* w8,
+                       int Cout, int KH, int KW, int stride, int pad, int dil, const float* bias,
+                       void* y, long long ldy, int OH, int OW, const float* x_state,
+                       const float* w_state, int nseg, float* ws, float* mean, float* invstd,
+                       float* run_mean, float* run_var, float momentum, float eps, hipStream_t stream);
 int cn_conv_fwd_bn(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
                    const void* w, int Cout, int KH, int KW, int stride, int pad, int dil,
                    const float* bias, void* y, long long ldy, int OH, int OW, int nseg, float* ws,

@@ -777,6 +777,41 @@ def test_conv_fwd_fp8(cuda, case):
     assert err <= 1e-2, err
 
 
+@pytest.mark.parametrize("case", [(2, 64, 13, 11, 128, 1, 1, 0, 1, 2), (2, 256, 17, 15, 256, 3, 1, 2, 2, 2),
+                                  (1, 128, 30, 30, 512, 3, 1, 6, 6, 1), (2, 512, 9, 9, 64, 1, 1, 0, 1, 2)])
+def test_conv_fwd_fp8_bn_epilogue_stats(cuda, case):
+    """cn_conv_fwd_fp8_bn (configs[4]): the fp8 conv's output equals cn_conv_fwd_fp8's BITWISE
+    (same kernel, EPI 1 only adds the reduction), and the per-segment batch statistics come out of
+    the epilogue equal to fp64 statistics of that stored output (running stats in segment order)."""
+    n, cin, h, w, cout, k, s, p, d, nseg = case
+    x = rnd((nseg * n, cin, h, w), torch.float32, 41, scale=2.0) + 1.0
+    wt = rnd((cout, cin, k, k), torch.float32, 42, scale=(2.0 / (cin * k * k)) ** 0.5)
+    xs, ws = ops.fp8_state(cuda), ops.fp8_state(cuda)
+    x8 = ops.fp8_quant(nhwc(x).float().to(cuda).contiguous(), xs, ops.FP8_CURRENT)
+    w8 = ops.fp8_quant(wt.permute(0, 2, 3, 1).reshape(cout * k * k, cin).float().to(cuda).contiguous(),
+                       ws, ops.FP8_CURRENT).view(cout, k * k * cin)
+    bias = rnd((cout,), torch.float32, 43, scale=0.5).float().to(cuda)
+    bn = _BN(cout, cuda, 44)
+    y0, oh, ow = ops.conv_fwd_fp8(x8, nseg * n, h, w, w8, cout, k, s, p, d, xs, ws, bias=bias)
+    y, oh, ow, (mean, invstd) = ops.conv_fwd_fp8_bn(x8, nseg * n, h, w, w8, cout, k, s, p, d, xs, ws,
+                                                    bn, nseg, bias=bias)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    yr = nchw(y, nseg * n, oh, ow).double().cpu()
+    rm, rv = torch.zeros(cout, dtype=torch.float64), torch.ones(cout, dtype=torch.float64)
+    for sg in range(nseg):
+        ys = yr[sg * n:(sg + 1) * n]
+        mu = ys.mean(dim=(0, 2, 3))
+        var = ys.var(dim=(0, 2, 3), unbiased=False)
+        cnt = ys.numel() // cout
+        assert torch.allclose(mean[sg * cout:(sg + 1) * cout].double().cpu(), mu, atol=1e-4 * (1 + mu.abs().max().item()), rtol=1e-5)
+        assert torch.allclose(invstd[sg * cout:(sg + 1) * cout].double().cpu(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4)
+        rm = 0.9 * rm + 0.1 * mu
+        rv = 0.9 * rv + 0.1 * var * cnt / (cnt - 1)
+    assert torch.allclose(bn.running_mean.double().cpu(), rm, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(bn.running_var.double().cpu(), rv, rtol=1e-4, atol=1e-5)
+
+
 def _dec_e5m2(y8):
     return y8.cpu().view(torch.float8_e5m2).double()
 
