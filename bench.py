@@ -292,7 +292,12 @@ def extra_line(dev, B, S, kind, steps=5, warmup=2):
            "model_tflops_per_s": B * steps * FLOP_PER_PAIR_473 / dt / 1e12 if S == 473 else None}
     if kind == "fp32":
         out["peak_tflops"] = MFMA_F32_PEAK_TFLOPS
+    # the model and its step hold reference cycles (encoder <-> deferred-backward holder, the
+    # recording's tensors): collect them, or each extra line leaves ~10 GB reserved
+    # (profiles/r06_bench_order_probe.txt)
     del st, opt, m
+    import gc
+    gc.collect()
     torch.cuda.empty_cache()
     return out
 
