@@ -46,6 +46,8 @@ _SIGS = {
     "cn_conv_fwd_fp8": (_I, [_P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I, _P,
                              _P, _P]),
     "cn_conv_fwd_bn_workspace_floats": (_S, [_I, _I, _I, _I]),
+    "cn_conv_fwd_bn_grouped": (_I, [_I, _P, _L, _I, _I, _I, _I, _I, _P, _I, _I, _I, _P, _P, _P, _L, _I,
+                                    _P, _P, _P, _P, _P, _F, _F, _P]),
     "cn_conv_fwd_fp8_bn": (_I, [_P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I,
                                 _P, _P, _I, _P, _P, _P, _P, _P, _F, _F, _P]),
     "cn_conv_fwd_bn": (_I, [_I, _P, _L, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _L, _I, _I,

@@ -286,6 +286,53 @@ extern "C" int cn_conv_fwd_fp8_bn(const void* x8, long long ldx, int N, int H, i
                                run_var, momentum, eps, st);
 }
 
+// G stride-1 'same' convs of one input x and one shape that differ in dilation (pad = dil), bias
+// and weights -- the ASPP's atrous branches (deeplab/deeplabv3_encoder.py:22-31, :70-76) -- as ONE
+// grouped GEMM launch (blockIdx.z = branch) with the BN-statistics epilogue of cn_conv_fwd_bn per
+// branch.  The branches' launches are each one round of the chip whose time the tiles without
+// tap skipping set (§3.1); grouped, their tiles share the rounds.  w, bias, y, ws, mean, invstd,
+// run_mean, run_var, dil: host arrays of G entries (device pointers / ints); ws[g]:
+// cn_conv_fwd_bn_workspace_floats(dtype, M, Cout, K) floats each.  G <= 24.
+extern "C" int cn_conv_fwd_bn_grouped(int dtype, const void* x, long long ldx, int N, int H, int W,
+                                      int Cin, int G, const void* const* w, int Cout, int KH, int KW,
+                                      const int* dil, const float* const* bias, void* const* y,
+                                      long long ldy, int nseg, float* const* ws, float* const* mean,
+                                      float* const* invstd, float* const* run_mean,
+                                      float* const* run_var, float momentum, float eps, hipStream_t st) {
+  if (G < 1 || G > GEMM_MAXG || KH != KW || KH % 2 == 0) return CN_ERR_SHAPE;
+  GemmArgs a;
+  int la;
+  const int d0 = dil[0], p0 = d0 * (KH / 2);
+  int rc = conv_fwd_args(dtype, x, ldx, N, H, W, Cin, w[0], Cout, KH, KW, 1, p0, d0, bias[0], y[0],
+                         ldy, H, W, a, la);
+  if (rc) return rc;
+  if (la != L_KC_CONV || nseg < 1 || a.M % nseg) return CN_ERR_SHAPE;
+  const int bm = cn_gemm_bm(dtype, a.M, a.N, a.K, -1);
+  const long long mt = (a.M + bm - 1) / bm;
+  a.ngroup = G;
+  for (int g = 0; g < G; ++g) {
+    if (dil[g] < 1 || !ws[g]) return CN_ERR_SHAPE;
+    a.grp.A[g] = x;
+    a.grp.B[g] = w[g];
+    a.grp.C[g] = y[g];
+    a.grp.bias[g] = bias[g];
+    a.grp.ST[g] = ws[g];
+    a.grp.dil[g] = dil[g];
+  }
+  a.st_mode = 1;
+  a.st_ws = ws[0];
+  a.st_plane = mt * Cout;
+  a.st_seg_rows = a.M / nseg;
+  rc = cn_gemm_dispatch(a, dtype, 0, la, L_KC_DENSE, G, st);
+  if (rc) return rc;
+  for (int g = 0; g < G; ++g) {
+    rc = cn_bn_tile_stats_impl(ws[g], a.st_plane, (int)mt, bm, a.M, nseg, Cout, mean[g], invstd[g],
+                               run_mean[g], run_var[g], momentum, eps, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 extern "C" size_t cn_conv_dgrad_bn_workspace_floats(int dtype, int M, int Cin, int K) {
   return (size_t)2 * mtiles_of(dtype, M, Cin, K) * Cin;
 }

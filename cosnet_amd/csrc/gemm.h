@@ -32,6 +32,12 @@ struct GemmGroup {
   // fp8 operands: per-problem dequantisation scales (null: the launch-wide scale_a / scale_b)
   const float* SA[GEMM_MAXG];
   const float* SB[GEMM_MAXG];
+  // grouped convs that differ in more than their operands (round 6, the ASPP's atrous branches):
+  // per-problem bias, BN-statistics workspace (EPI 1) and dilation of the A gather (> 0: the
+  // gather's offset / step become -dil / +dil, 'same' padding); null / 0: the launch-wide ones
+  const float* bias[GEMM_MAXG];
+  float* ST[GEMM_MAXG];
+  int dil[GEMM_MAXG];
 };
 
 struct GemmArgs {

@@ -497,6 +497,16 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   const int batch = bz / p.nsplit, split = bz - batch * p.nsplit;
   int kbeg = split * p.k_chunk;
   int kend = min(p.K, kbeg + p.k_chunk);
+  // the A gather's geometry: per problem in a grouped launch of convs of different dilations
+  ConvGeom gA = p.ga;
+  if constexpr (LA == L_KC_CONV) {
+    if (p.ngroup && p.grp.dil[batch] > 0) {
+      const int dl = p.grp.dil[batch];
+      gA.off_y = gA.off_x = -dl;
+      gA.step_y = gA.step_x = dl;
+    }
+  }
+  const float* bias = (p.ngroup && p.grp.bias[batch]) ? p.grp.bias[batch] : p.bias;
   if constexpr (LA == L_KC_CONV) {
     // Vertical tap skipping (conv forward / stride-1 dgrad gathers; k = (r, s, ci), r-major): the
     // taps r whose source rows y = oy st + off_y + r step_y miss the image for EVERY row of this
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
     // where a 256-row tile (~4 image rows) near the top or bottom edge has a whole tap row of
     // padding.  Uniform per block (the tile's first / last row); a tile spanning two images
     // keeps every tap.
-    const ConvGeom& g = p.ga;
+    const ConvGeom& g = gA;
     if (g.KH > 1) {
       int i0, i1, rm0, rm1, oy0, oy1, ox;
       fdivmod(m0, g.div_OHW, i0, rm0);
@@ -531,7 +541,7 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
 
   LdA la;
   LdB lb;
-  la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), p.ga, m0, tid, kbeg);
+  la.init(Abase, p.lda, p.M, min(p.ka_lim, kend), gA, m0, tid, kbeg);
   lb.init(Bbase, p.ldb, p.N, min(p.kb_lim, kend), p.gb, n0, tid, kbeg);
 
   // Epilogue geometry (below) and the epilogue operands that do not depend on the product,
@@ -881,7 +891,7 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = n0 + c0t + e;
-        sk[e] = cs[c0t + e] + ((p.bias && c < p.N) ? p.bias[c] : 0.f);
+        sk[e] = cs[c0t + e] + ((bias && c < p.N) ? bias[c] : 0.f);
       }
     }
 #pragma unroll
@@ -904,9 +914,9 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
       *(f32x4*)&v[4] = *(const f32x4*)&cs[rr * LDC + c0 + 4];
       CT* dst = Cb + drow * p.ldc + col;
       const bool full = col + 8 <= p.N && ((uintptr_t)dst % 16 == 0);
-      if (p.bias) {
+      if (bias) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (col + e < p.N) ? p.bias[col + e] : 0.f;
+        for (int e = 0; e < 8; ++e) v[e] += (col + e < p.N) ? bias[col + e] : 0.f;
       }
       if (cmode == 1) {
 #pragma unroll
@@ -1004,7 +1014,7 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
       }
     }
     __syncthreads();
-    float* ws = p.st_ws + (long long)tm * p.N;
+    float* ws = ((p.ngroup && p.grp.ST[batch]) ? p.grp.ST[batch] : p.st_ws) + (long long)tm * p.N;
     for (int t = tid; t < nq * BN; t += NT) {
       const int q = t / BN, c = t % BN;
       float a = 0.f;
@@ -1121,24 +1131,24 @@ static int launch_c(const GemmArgs& a, int batch, hipStream_t st) {
 // BN-epilogue GEMMs (conv fwd with statistics, stride-1 dgrad with the BN backward reduce):
 // only the tiles the shape heuristic picks for conv fwd / dgrad are instantiated.
 template <class T, int LA, int EPI>
-static int launch_epi(const GemmArgs& a, hipStream_t st) {
+static int launch_epi(const GemmArgs& a, int batch, hipStream_t st) {
   if constexpr (sizeof(T) == 4) {
-    if (a.N <= 64 || cfg_blocks(1, a, 1) < 384) return launch_c<T, T, 0, LA, L_KC_DENSE, EPI>(a, 1, st);
-    return launch_c<T, T, 1, LA, L_KC_DENSE, EPI>(a, 1, st);
+    if (a.N <= 64 || cfg_blocks(1, a, batch) < 384) return launch_c<T, T, 0, LA, L_KC_DENSE, EPI>(a, batch, st);
+    return launch_c<T, T, 1, LA, L_KC_DENSE, EPI>(a, batch, st);
   } else {
-    switch (pick_cfg(a, 1)) {
-      case 10: return launch_c<T, T, 10, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 11: return launch_c<T, T, 11, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 12: return launch_c<T, T, 12, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 13: return launch_c<T, T, 13, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 18: return launch_c<T, T, 18, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 19: return launch_c<T, T, 19, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 20: return launch_c<T, T, 20, LA, L_KC_DENSE, EPI>(a, 1, st);
+    switch (pick_cfg(a, batch)) {
+      case 10: return launch_c<T, T, 10, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 11: return launch_c<T, T, 11, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 12: return launch_c<T, T, 12, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 13: return launch_c<T, T, 13, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 18: return launch_c<T, T, 18, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 19: return launch_c<T, T, 19, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 20: return launch_c<T, T, 20, LA, L_KC_DENSE, EPI>(a, batch, st);
 #if CN_EXPERIMENTAL
-      case 21: return launch_c<T, T, 21, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 22: return launch_c<T, T, 22, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 24: return launch_c<T, T, 24, LA, L_KC_DENSE, EPI>(a, 1, st);
-      case 25: return launch_c<T, T, 25, LA, L_KC_DENSE, EPI>(a, 1, st);
+      case 21: return launch_c<T, T, 21, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 22: return launch_c<T, T, 22, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 24: return launch_c<T, T, 24, LA, L_KC_DENSE, EPI>(a, batch, st);
+      case 25: return launch_c<T, T, 25, LA, L_KC_DENSE, EPI>(a, batch, st);
 #endif
       default: return CN_ERR_UNSUPPORTED;
     }
@@ -1326,12 +1336,13 @@ int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, in
     return CN_ERR_UNSUPPORTED;
   }
   if (a.st_mode) {
-    if (batch != 1 || a.nsplit != 1 || a.row_map || a.c_mode ||
+    // grouped (EPI 1 only): one problem per blockIdx.z, each with its own statistics workspace
+    if ((batch != 1 && !(a.ngroup == batch && a.st_mode == 1)) || a.nsplit != 1 || a.row_map || a.c_mode ||
         lb != L_KC_DENSE || (la != L_KC_DENSE && la != L_KC_CONV && la != L_KC_CONV_G))
       return CN_ERR_UNSUPPORTED;
 #define CN_EPI(T_, M_) \
-    return la == L_KC_DENSE ? launch_epi<T_, L_KC_DENSE, M_>(a, st) : \
-           la == L_KC_CONV ? launch_epi<T_, L_KC_CONV, M_>(a, st) : launch_epi<T_, L_KC_CONV_G, M_>(a, st)
+    return la == L_KC_DENSE ? launch_epi<T_, L_KC_DENSE, M_>(a, batch, st) : \
+           la == L_KC_CONV ? launch_epi<T_, L_KC_CONV, M_>(a, batch, st) : launch_epi<T_, L_KC_CONV_G, M_>(a, batch, st)
     if (dtype == DT_BF16) {
       if (a.st_mode == 1) CN_EPI(bf16, 1); else CN_EPI(bf16, 2);
     } else {

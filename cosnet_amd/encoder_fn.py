@@ -60,9 +60,16 @@ WGRAD_GSPLIT = int(os.environ.get("CN_WGRAD_GSPLIT", "512"))
 # fp8 mode (configs[4]): the 3x3 bottleneck and ASPP weight gradients on fp8 operands
 # (cn_conv_wgrad_fp8); CN_WGRAD_FP8=0 keeps them bf16 (A/B runs).
 WGRAD_FP8 = os.environ.get("CN_WGRAD_FP8", "1") != "0"
+# The ASPP's three atrous convs in one grouped launch (cn_conv_fwd_bn_grouped, train mode, bf16 /
+# fp32): measured level with the three launches in the two-stream step (the depth stream already
+# fills the CUs a one-round launch leaves idle; profiles/r06_aspp_grouped_fp8_stats_ab.txt), so
+# off by default; CN_ASPP_GROUPED=1 selects it.
+ASPP_GROUPED = os.environ.get("CN_ASPP_GROUPED", "0") == "1"
 # fp8 mode: the BN statistics of the long-K narrow fp8 convs (fuse_stats) from the fp8 GEMM's
-# epilogue (cn_conv_fwd_fp8_bn) instead of their own pass; CN_FP8_FUSE_STATS=0 for A/B runs.
-FP8_FUSE_STATS = os.environ.get("CN_FP8_FUSE_STATS", "1") != "0"
+# epilogue (cn_conv_fwd_fp8_bn) instead of their own pass: measured 0.8 % SLOWER on the configs[4]
+# step (the fp8 tiles' epilogue is long next to their K loop), so off by default;
+# CN_FP8_FUSE_STATS=1 selects it.
+FP8_FUSE_STATS = os.environ.get("CN_FP8_FUSE_STATS", "0") == "1"
 # TIMING PROBE ONLY (results are wrong): CN_PROBE_SKIP_APPLY=1 / 2 / 3 drops the bn1 / bn2 / both
 # BN + ReLU apply passes of every bottleneck (the next conv reads the raw conv output) -- the
 # upper bound of what folding those applies into the consumer conv's operand path could save
@@ -449,12 +456,26 @@ def aspp_fwd(mod, x, geo, nseg, rec):
     convs = [(mod.conv2d_0, mod.bn_0, 1, 0)] + [
         (getattr(mod, "conv2d_%d" % (i + 1)), getattr(mod, "bn_%d" % (i + 1)), 3, dd)
         for i, dd in enumerate(mod.cn_dilations)]
+    # the atrous branches as one grouped launch (train mode, statistics from the epilogue, not
+    # fp8): each branch's launch alone is one round of the chip set by its tiles that skip no tap
+    grouped = {}
+    if (tr and ctx is None and ASPP_GROUPED and fuse_stats(512, 9 * x.shape[1])
+            and all(dd > 0 for (_, _, _, dd) in convs[1:])):
+        at = convs[1:]
+        outs = ops.conv_fwd_bn_grouped(x, n, h, w, [WCACHE.get(cm.weight, dt)[0] for (cm, _, _, _) in at],
+                                       512, 3, [dd for (_, _, _, dd) in at], [bnm for (_, bnm, _, _) in at],
+                                       nseg, biases=[cm.bias for (cm, _, _, _) in at])
+        for bi, (y_, st_) in enumerate(outs):
+            grouped[bi + 1] = (y_, SegStats(st_, nseg, 512))
     cs, sts, wts, q8s = [], [], [], []
     for bi, (cm, bnm, k, dd) in enumerate(convs):
         wf, wt = WCACHE.get(cm.weight, dt)
         q = [] if rec is not None and WGRAD_FP8 else None
-        ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias,
-                               weight=cm.weight, q8=q)
+        if bi in grouped:
+            ci, st = grouped[bi]
+        else:
+            ci, _, _, st = conv_bn(x, n, h, w, wf, 512, k, 1, dd, max(dd, 1), bnm, tr, nseg, bias=cm.bias,
+                                   weight=cm.weight, q8=q)
         q8s.append(q)
         sl = slice(512 * (bi + 1), 512 * (bi + 2))
         if cat8 is not None:

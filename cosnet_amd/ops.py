@@ -324,6 +324,39 @@ def conv_fwd_fp8(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, 
     return out, oh, ow
 
 
+def conv_fwd_bn_grouped(x, n, h, w, wfs, cout, k, dils, bns, nseg=1, biases=None):
+    """The ASPP's atrous branches as ONE grouped launch (cn_conv_fwd_bn_grouped): for each g,
+    y_g = conv(x, wfs[g], dilation dils[g], padding dils[g]) (+ biases[g]) and the BN batch
+    statistics of y_g from the GEMM epilogue (as conv_fwd_bn).  Returns [(y_g, (mean, invstd))]."""
+    import ctypes
+    G = len(wfs)
+    cin = wfs[0].shape[1] // (k * k)
+    M = n * h * w
+    if M % nseg or M // nseg <= 1:
+        raise ValueError("Expected more than 1 value per channel when training, got input size "
+                         "torch.Size([%d, %d, 1, 1])" % (M // nseg, cout))
+    dev = x.device
+    ys = [torch.empty((M, cout), dtype=x.dtype, device=dev) for _ in range(G)]
+    means = [torch.empty((nseg * cout,), dtype=torch.float32, device=dev) for _ in range(G)]
+    invs = [torch.empty_like(m) for m in means]
+    nws = int(nv.query("cn_conv_fwd_bn_workspace_floats", dtc(x), M, cout, k * k * cin))
+    wss = [torch.empty((nws,), dtype=torch.float32, device=dev) for _ in range(G)]
+    biases = biases or [None] * G
+    P = lambda ts: (ctypes.c_void_p * G)(*[t.data_ptr() if t is not None else None for t in ts])
+    es = x.element_size()
+    ev = _prof_start(2.0 * G * M * cout * k * k * cin, ("fwd", M, cout * G, k * k * cin),
+                     es * (n * h * w * cin + G * cout * k * k * cin + G * M * cout))
+    mom = bns[0].momentum if bns[0].momentum is not None else BN_MOMENTUM
+    nv.call("cn_conv_fwd_bn_grouped", dtc(x), x.data_ptr(), ld(x), n, h, w, cin, G, P(wfs), cout, k, k,
+            (ctypes.c_int * G)(*dils), P(biases), P(ys), cout, nseg, P(wss), P(means), P(invs),
+            P([b.running_mean for b in bns]), P([b.running_var for b in bns]), float(mom),
+            float(bns[0].eps), nv.stream())
+    _prof_end(ev)
+    for b in bns:
+        b._cn_nbt = getattr(b, "_cn_nbt", 0) + nseg
+    return [(y, (m, i)) for y, m, i in zip(ys, means, invs)]
+
+
 def conv_fwd_fp8_bn(x8, n, h, w, wf8, cout, k, stride, pad, dil, x_state, w_state, bn, nseg=1,
                     bias=None):
     """conv_fwd_fp8 + the BN batch statistics of its stored bf16 output from the GEMM epilogue

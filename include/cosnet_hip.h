@@ -143,6 +143,17 @@ int cn_conv_fwd_fp8(const void* x8, long long ldx, int N, int H, int W, int Cin,
  * [nseg][Cout]; running stats updated segment after segment (momentum, eps as nn.BatchNorm2d).
  * ws: cn_conv_fwd_bn_workspace_floats(dtype, M, Cout, KH*KW*Cin) floats. */
 size_t cn_conv_fwd_bn_workspace_floats(int dtype, int M, int Cout, int K);
+/* G stride-1 'same' convs (pad = dil[g]) of ONE input x and one shape, differing in weights,
+ * bias and dilation -- the ASPP's atrous branches (deeplab/deeplabv3_encoder.py:22-31, :70-76)
+ * -- as one grouped launch with cn_conv_fwd_bn's statistics epilogue per branch.  w, dil, bias,
+ * y, ws, mean, invstd, run_mean, run_var: host arrays of G (<= 24) entries; y[g] [N*H*W][ldy];
+ * ws[g]: cn_conv_fwd_bn_workspace_floats(dtype, M, Cout, KH*KW*Cin) floats. */
+int cn_conv_fwd_bn_grouped(int dtype, const void* x, long long ldx, int N, int H, int W, int Cin,
+                           int G, const void* const* w, int Cout, int KH, int KW, const int* dil,
+                           const float* const* bias, void* const* y, long long ldy, int nseg,
+                           float* const* ws, float* const* mean, float* const* invstd,
+                           float* const* run_mean, float* const* run_var, float momentum, float eps,
+                           hipStream_t stream);
 /* cn_conv_fwd_fp8 with the same BN-statistics epilogue (configs[4]: the fp8 forward convs whose
  * statistics the bf16 path also takes from the epilogue); ws: cn_conv_fwd_bn_workspace_floats(
  * 2 (fp8), M, Cout, K) floats.  Replaces nn.Conv2d + nn.BatchNorm2d's batch statistics as above. */

@@ -812,6 +812,37 @@ def test_conv_fwd_fp8_bn_epilogue_stats(cuda, case):
     assert torch.allclose(bn.running_var.double().cpu(), rv, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 256, 17, 15, 128, (1, 2, 5), 2), (1, 512, 30, 30, 512, (6, 12, 18), 1)])
+def test_conv_fwd_bn_grouped_is_the_separate_launches(cuda, dt, case):
+    """cn_conv_fwd_bn_grouped (the ASPP's atrous branches in one launch: per-problem weights,
+    bias, dilation and statistics workspace) is BITWISE the G separate cn_conv_fwd_bn launches --
+    outputs, batch statistics and running-stat updates -- and those are pinned to fp64 by
+    test_conv_fwd_bn_epilogue_stats."""
+    n, cin, h, w, cout, dils, nseg = case
+    G = len(dils)
+    x = rnd((nseg * n, cin, h, w), dt, 51, scale=2.0) + 1.0
+    xg = nhwc(x).to(dt).to(cuda).contiguous()
+    wfs, biases = [], []
+    for g in range(G):
+        wt = rnd((cout, cin, 3, 3), dt, 52 + g, scale=(2.0 / (cin * 9)) ** 0.5)
+        wfs.append(wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin).to(dt).to(cuda).contiguous())
+        biases.append(rnd((cout,), torch.float32, 60 + g, scale=0.5).float().to(cuda))
+    bns_a = [_BN(cout, cuda, 70 + g) for g in range(G)]
+    bns_b = [_BN(cout, cuda, 70 + g) for g in range(G)]
+    outs = ops.conv_fwd_bn_grouped(xg, nseg * n, h, w, wfs, cout, 3, list(dils), bns_a, nseg, biases=biases)
+    refs = [ops.conv_fwd_bn(xg, nseg * n, h, w, wfs[g], cout, 3, 1, dils[g], dils[g], bns_b[g], nseg,
+                            bias=biases[g]) for g in range(G)]
+    torch.cuda.synchronize()
+    for g in range(G):
+        y, (m, i) = outs[g]
+        yr, _, _, (mr, ir) = refs[g]
+        assert torch.equal(y, yr), g
+        assert torch.equal(m, mr) and torch.equal(i, ir), g
+        assert torch.equal(bns_a[g].running_mean, bns_b[g].running_mean), g
+        assert torch.equal(bns_a[g].running_var, bns_b[g].running_var), g
+
+
 def _dec_e5m2(y8):
     return y8.cpu().view(torch.float8_e5m2).double()
 
