@@ -688,10 +688,20 @@ int coatt_q48_launch(int mode, FusedArgs& a, int B, int nd, bool merge_ok, void*
     a.opart = (float*)ws;                  // bf16 rows of FD channels
     a.mlpart = a.opart + rows * FD / 2;
     a.cnt = (int*)(a.mlpart + rows * 2);
-    // zeroed by a kernel, not hipMemsetAsync: inside a recorded step that is a kernel node like
-    // every other (no memset nodes in the captured graphs); the merge resets each counter too
-    hipLaunchKernelGGL(q48_zero_cnt_k, dim3(1), dim3(256), 0, st, a.cnt, a.nitems);
-    CN_CHECK_LAUNCH();
+    // zeroed by hipMemsetAsync (the merge resets each counter too).  Round 6 measured the
+    // alternative the advisor suggested -- a one-workgroup zeroing kernel, a kernel node instead
+    // of a memset node in the recorded step -- at 2.7 % of the whole training step: 132.1 vs 135.7
+    // frame-pairs/s, the training co-attention 0.16 vs 0.21 of peak, each forward launch ~70 us
+    // longer in HIP events (profiles/r06_q48_counter_zero_ab.txt).  CN_Q48_ZERO_KERNEL=1 selects
+    // the kernel (A/B runs).
+    static const bool use_kernel = [] { const char* e = getenv("CN_Q48_ZERO_KERNEL"); return e && e[0] == '1'; }();
+    if (!use_kernel) {
+      const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)a.nitems * sizeof(int), st);
+      if (e != hipSuccess) return (int)e;
+    } else {
+      hipLaunchKernelGGL(q48_zero_cnt_k, dim3(1), dim3(256), 0, st, a.cnt, a.nitems);
+      CN_CHECK_LAUNCH();
+    }
   }
   if (mode == 0) hipLaunchKernelGGL(coatt_q48_k<0>, dim3(a.nwork), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(coatt_q48_k<1>, dim3(a.nwork), dim3(256), 0, st, a);

@@ -39,7 +39,8 @@ def _bufs(st):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, "fp8"])
 def test_graph_step_matches_eager(cuda, dtype, mode):
     """Graph replays follow the eager trajectory BIT FOR BIT: every reduction of the step is a
-    fixed-order sum (no float atomics, no memset nodes), so two eager runs are bitwise
+    fixed-order sum (no float atomics; the co-attention's stream-K counters are memset nodes
+    that only order the merge, not its sum), so two eager runs are bitwise
     identical, and so is the replayed graph -- losses, every SGD momentum buffer (the running
     sum of each parameter's gradients, so a gradient contribution missing from the recording
     shows up) and the BN running statistics.  mode "one": the step as one recorded graph; "split":
