@@ -16,6 +16,7 @@
 #   smoke            __graft_entry__.smoke()
 #   py:SCRIPT[,ARGS] python SCRIPT ARGS (a tools/ probe or A/B script)
 #   envbench:VAR=VALUE[,ARGS]  bench.py ARGS with one environment variable set (A/B lines)
+#   envprof:VAR=VALUE[,ARGS]   the prof step with one environment variable set (into prof_<i>/)
 set -o pipefail
 NAME=$1; shift
 O=gpurun_out/$NAME
@@ -42,6 +43,13 @@ for step in "$@"; do
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
         python3 bench.py --steps 8 --warmup 3 --cpu-baseline 0 --fp32-extra 0 --fp8-extra 0 ${arg//,/ } > $O/prof.log 2>&1
+      rc=$?; note "$step rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    envprof)
+      # envprof:VAR=VALUE[,ARGS]  the prof step with one environment variable set (rocprofv3 takes
+      # the program itself after --, so the variable is exported for this step only)
+      ev=${arg%%,*}; rest=${arg#*,}; [ "$rest" = "$arg" ] && rest=""
+      ( export "$ev"; timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$i -o run -- \
+        python3 bench.py --steps 8 --warmup 3 --cpu-baseline 0 --fp32-extra 0 --fp8-extra 0 ${rest//,/ } > $O/prof_$i.log 2>&1 )
       rc=$?; note "$step rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       timeout -k 10 600 bash tools/pmc_run.sh $O/pmc > $O/pmc.log 2>&1
