@@ -44,6 +44,12 @@ from . import _native as nv
 from . import functions as fn
 from . import ops
 
+# Stream capture checks only the recording thread: with an nccl (RCCL) process group, its
+# watchdog thread polls the events of finished all-reduces at any time, and under the default
+# "global" mode one such poll landing inside a recording aborts the process (seen under rocprofv3,
+# whose slower start moved the poll into the capture window).  Nothing else runs in other threads.
+CAPTURE_MODE = "thread_local"
+
 
 class TrainStep:
     """`size` = H (square frames) or (H, W); `batch` = frame pairs on this rank."""
@@ -296,7 +302,8 @@ class TrainStep:
         for op in prog:
             if op[0] == "run":
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=S[op[1]], pool=pools[op[1]]):
+                with torch.cuda.graph(g, stream=S[op[1]], pool=pools[op[1]],
+                                      capture_error_mode=CAPTURE_MODE):
                     op[2]()
                 rec.append(("graph", op[1], g))
             else:
@@ -470,7 +477,7 @@ class TrainStep:
                 self._record_program()
             else:
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph, stream=s):
+                with torch.cuda.graph(self.graph, stream=s, capture_error_mode=CAPTURE_MODE):
                     self._body()
         finally:
             self._capturing = False
