@@ -17,6 +17,7 @@ TRAIN = ("coatt_fused_fwd_k", "coatt_q48_k", "coatt_flash_dvat_k", "dvat_sum_k",
 FWD0 = ("coatt_fused_fwd_k<0>", "coatt_merge_k<0>", "coatt_q48_k<0>")
 PV = ("coatt_fused_fwd_k<1>", "coatt_merge_k<1>", "coatt_q48_k<1>", "dvat_sum_k")
 MAIN0 = ("coatt_fused_fwd_k<0>", "coatt_q48_k<0>")
+TIMED = 200   # bench.py coattention_roofline: 5 x (graph replay of 20 + 20 eager launches)
 
 
 def summarise(path):
@@ -48,7 +49,12 @@ def summarise(path):
             "train_families": {k: {"launches_per_step": v[0] / steps, "us_per_step": v[1] / steps}
                                for k, v in sorted(fam.items())},
             "configs3_launches": len(c3_main),
-            "configs3_us_per_launch": (sum(dur(r) for r in c3) / len(c3_main)) if c3_main else None}
+            "configs3_us_per_launch": (sum(dur(r) for r in c3) / len(c3_main)) if c3_main else None,
+            # the timed part of bench.py's configs[3] line (round 6: settling replays first, then 5
+            # x (graph of 20 + 20 eager launches)): its last TIMED launches
+            "configs3_timed_launches": min(len(c3_main), TIMED),
+            "configs3_us_per_launch_timed": (sum(dur(r) for r in c3_main[-TIMED:]) /
+                                             min(len(c3_main), TIMED)) if c3_main else None}
 
 
 if __name__ == "__main__":
