@@ -259,9 +259,10 @@ def coattention_roofline(dev, n=5, hw=3600, c=256, iters=20):
             torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e-3 / iters
 
-    # settle: this line runs right after the training lines, and the kernel keeps speeding up for
-    # tens of ms after them (162 -> 144 us per launch over ~20 ms in a trace: the clocks recover
-    # from the training step's load) -- replay until two replays in a row agree within 1 %
+    # settle: after the gap this line's setup leaves, the kernel speeds up for tens of ms (170 ->
+    # 145 us per launch over ~30 ms, graph or eager alike) while the reported gfx / memory clocks
+    # stay put and the socket power climbs (profiles/r06_clock_probe.txt) -- a warm-up below what
+    # amdsmi reports; replay until two replays in a row agree within 1 %
     first = prev = replay()
     settle = 1
     while settle < 60:
