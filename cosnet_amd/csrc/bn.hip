@@ -43,6 +43,27 @@ template <class T> __device__ __forceinline__ void ld_chunk(const T* p, float* f
 template <class T> __device__ __forceinline__ void st_chunk(T* p, const float* f) {
   *(u32x4*)p = Chunk<T>::pack(f);
 }
+// the same chunk stored write-through (sc1) at a byte offset from a buffer resource's base
+template <class T> __device__ __forceinline__ void st_chunk_wt(__amdgpu_buffer_rsrc_t r, long long off,
+                                                              const float* f) {
+  __builtin_amdgcn_raw_buffer_store_b128(Chunk<T>::pack(f), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+// The apply kernels store their outputs write-through (sc1) where the byte offsets from the
+// output's base fit 31 bits: the lines go to memory as they are written instead of waiting dirty
+// in the XCD's L2 for the end-of-kernel write-back that the next kernel's start waits on
+// (+0.55 % on the step; the same for the GEMM epilogue's C stores measured -0.4 %:
+// profiles/r06_write_through_ab.txt).  CN_BN_WT=0: plain stores; 2: also the ReLU-mask bytes and
+// the fp8 output copy (A/B runs).
+static int bn_wt_env() {
+  static const int lvl = [] { const char* e = getenv("CN_BN_WT"); return e ? atoi(e) : 1; }();
+  return lvl;
+}
+static int bn_wt(long long rows, long long ld, int esz) {
+  return rows * ld * esz < 0x7fff0000ll ? bn_wt_env() : 0;
+}
 
 // Column sums of the block's RPB rows of per-thread accumulators, written as
 // out[q][blockIdx.y][c] (q < NQ planes of S x C floats).  Parallel over all 256 threads: with
@@ -344,8 +365,11 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
                                                   const float* prelu, T* __restrict__ y,
                                                   long long ldy, unsigned char* __restrict__ y8,
                                                   long long ldy8, float* qstate,
-                                                  unsigned char* __restrict__ mk, long long ldm) {
+                                                  unsigned char* __restrict__ mk, long long ldm,
+                                                  int wt) {
   constexpr int V = VecOf<T>::N;
+  // wt: y stored write-through (sc1), offsets from y (the host checked they fit 31 bits)
+  const __amdgpu_buffer_rsrc_t yrs = wt_rsrc(y), mkrs = wt_rsrc(mk), y8rs = wt_rsrc(y8);
   const Layout L = layout_of<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
@@ -405,14 +429,20 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         f[u][v] = t;
       }
       const u32x4 pk = Chunk<T>::pack(f[u]);
-      *(u32x4*)(y + r * ldy + c0) = pk;
+      if (wt)
+        __builtin_amdgcn_raw_buffer_store_b128(pk, yrs, (int)((r * ldy + c0) * (long long)sizeof(T)), 0, 16);
+      else
+        *(u32x4*)(y + r * ldy + c0) = pk;
       if (mk) {  // ReLU mask of the STORED values, one bit per channel (the backward's act 4)
         float sv[V];
         Chunk<T>::unpack(pk, sv);
         unsigned bits = 0;
 #pragma unroll
         for (int v = 0; v < V; ++v) bits |= (sv[v] > 0.f ? 1u : 0u) << v;
-        mk[r * ldm + chunk] = (unsigned char)bits;
+        if (wt > 1)
+          __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mkrs, (int)(r * ldm + chunk), 0, 16);
+        else
+          mk[r * ldm + chunk] = (unsigned char)bits;
       }
       if (y8) {  // fp8 copy of the output for an fp8 consumer conv (delayed scaling)
 #pragma unroll
@@ -422,7 +452,10 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
           u32x2 o;
           o.x = pack4_fp8_bn(f[u][v] * qinv, f[u][v + 1] * qinv, f[u][v + 2] * qinv, f[u][v + 3] * qinv);
           o.y = pack4_fp8_bn(f[u][v + 4] * qinv, f[u][v + 5] * qinv, f[u][v + 6] * qinv, f[u][v + 7] * qinv);
-          *(u32x2*)(y8 + r * ldy8 + c0 + v) = o;
+          if (wt > 1)
+            __builtin_amdgcn_raw_buffer_store_b64(o, y8rs, (int)(r * ldy8 + c0 + v), 0, 16);
+          else
+            *(u32x2*)(y8 + r * ldy8 + c0 + v) = o;
         }
       }
     }
@@ -539,8 +572,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
                                                       const float* prelu, const float* sum_dz,
                                                       const float* sum_dzxh, T* __restrict__ dx,
                                                       long long lddx, T* __restrict__ dres,
-                                                      long long lddres) {
+                                                      long long lddres, int wt) {
   constexpr int V = VecOf<T>::N;
+  const __amdgpu_buffer_rsrc_t dxr = wt_rsrc(dx), drr = wt_rsrc(dres);
   const Layout L = layout_of<T>(C);
   const int tx = threadIdx.x % L.CB, ty = threadIdx.x / L.CB;
   const int chunk = blockIdx.x * L.CB + tx;
@@ -610,8 +644,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
         o[v] = k1[v] * (dd - m1[v] - xh * m2[v]);
         d[u][v] = dd;
       }
-      st_chunk(dx + (long long)r * lddx + chunk * V, o);
-      if (dres) st_chunk(dres + (long long)r * lddres + chunk * V, d[u]);
+      if (wt) {
+        st_chunk_wt<T>(dxr, ((long long)r * lddx + chunk * V) * (long long)sizeof(T), o);
+        if (dres) st_chunk_wt<T>(drr, ((long long)r * lddres + chunk * V) * (long long)sizeof(T), d[u]);
+      } else {
+        st_chunk(dx + (long long)r * lddx + chunk * V, o);
+        if (dres) st_chunk(dres + (long long)r * lddres + chunk * V, d[u]);
+      }
     }
   }
 }
@@ -739,13 +778,13 @@ extern "C" int cn_bn_bwd_apply(int dtype, const void* x, long long ldx, const vo
     hipLaunchKernelGGL(bn_bwd_apply_k<bf16>, dim3(gx, gy), dim3(256), 0, st, (const bf16*)x, ldx,
                        (const bf16*)dy, lddy, (const bf16*)nullptr, 0ll, (const unsigned char*)nullptr, P, C, mean, invstd, gamma,
                        beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (bf16*)dx, lddx,
-                       (bf16*)nullptr, 0ll);
+                       (bf16*)nullptr, 0ll, bn_wt(P, lddx, 2));
   } else {
     gy = grid_rows<float>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
     hipLaunchKernelGGL(bn_bwd_apply_k<float>, dim3(gx, gy), dim3(256), 0, st, (const float*)x, ldx,
                        (const float*)dy, lddy, (const float*)nullptr, 0ll, (const unsigned char*)nullptr, P, C, mean, invstd, gamma,
                        beta, 3, (const float*)nullptr, sum_dz, sum_dzxh, (float*)dx, lddx,
-                       (float*)nullptr, 0ll);
+                       (float*)nullptr, 0ll, bn_wt(P, lddx, 4));
   }
   CN_CHECK_LAUNCH();
   return 0;
@@ -803,19 +842,22 @@ extern "C" int cn_bn_apply_ex(int dtype, const void* x, long long ldx, int P, in
       !aligned16(rmean) || !aligned16(rinvstd) || !aligned16(rgamma) || !aligned16(rbeta))
     return CN_ERR_ALIGN;
   if (P < 1 || nseg < 1) return CN_ERR_SHAPE;
+  int wt = bn_wt((long long)nseg * P, ldy, dtype == DT_BF16 ? 2 : 4);
+  if (wt > 1 && ((mask && !bn_wt((long long)nseg * P, ldm, 1)) || (y8 && !bn_wt((long long)nseg * P, ldy8, 1))))
+    wt = 1;
   int gx, gy;
   if (dtype == DT_BF16) {
     gy = grid_rows<bf16>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
     hipLaunchKernelGGL(bn_apply_k<bf16>, dim3(gx, gy, nseg), dim3(256), 0, st, (const bf16*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const bf16*)res, ldr, (const bf16*)xr, ldxr, rmean,
                        rinvstd, rgamma, rbeta, act, prelu, (bf16*)y, ldy, (unsigned char*)y8, ldy8,
-                       qstate, mask, ldm);
+                       qstate, mask, ldm, wt);
   } else {
     gy = grid_rows<float>(P, C, &gx, g_tune[T_AP_ROWS], g_tune[T_AP_BLOCKS], nseg);
     hipLaunchKernelGGL(bn_apply_k<float>, dim3(gx, gy, nseg), dim3(256), 0, st, (const float*)x, ldx, P, C,
                        mean, invstd, gamma, beta, (const float*)res, ldr, (const float*)xr, ldxr,
                        rmean, rinvstd, rgamma, rbeta, act, prelu, (float*)y, ldy,
-                       (unsigned char*)nullptr, 0ll, (float*)nullptr, mask, ldm);
+                       (unsigned char*)nullptr, 0ll, (float*)nullptr, mask, ldm, wt);
   }
   CN_CHECK_LAUNCH();
   return 0;
@@ -847,7 +889,8 @@ static int bn_bwd_launch(const T* x, long long ldx, const T* dy, long long lddy,
   if (!dx) return 0;
   gy = grid_rows<T>(P, C, &gx, g_tune[T_BA_ROWS], g_tune[T_BA_BLOCKS]);
   hipLaunchKernelGGL(bn_bwd_apply_k<T>, dim3(gx, gy), dim3(256), 0, st, x, ldx, dy, lddy, y, ldy, mk, P,
-                     C, mean, invstd, gamma, beta, act, prelu, dbeta, dgamma, dx, lddx, dres, lddres);
+                     C, mean, invstd, gamma, beta, act, prelu, dbeta, dgamma, dx, lddx, dres, lddres,
+                     bn_wt(P, lddx, (int)sizeof(T)) && (!dres || bn_wt(P, lddres, (int)sizeof(T))));
   CN_CHECK_LAUNCH();
   return 0;
 }

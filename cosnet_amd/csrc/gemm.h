@@ -75,6 +75,7 @@ struct GemmArgs {
   const float* br_mean; const float* br_invstd; const float* br_gamma; const float* br_beta;
   int ngroup;                  // > 0: grouped launch (GemmGroup), batch = ngroup, nsplit 1
   GemmGroup grp;
+  int wt;                      // C stores write-through (sc1): set by cn_gemm_dispatch
 };
 
 int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st);

@@ -569,6 +569,8 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
   CT* Cb = (p.ngroup ? (CT*)p.grp.C[batch] : (CT*)p.C + (long long)batch * p.c_bs) +
            (p.c_mode == 3 ? (long long)split * p.slab : 0);
   u32x4 xnx[(smode == 2 || PFC) ? IT * PQ : 1];   // the next staging pass's rows
+  // write-through C stores (p.wt): the block's rows from its first one, 32-bit offsets
+  const __amdgpu_buffer_rsrc_t crs = buf_rsrc(Cb + (long long)m0 * p.ldc);
   auto epi_fetch = [&](int pass) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -932,7 +934,10 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
             for (int e = 0; e < 8; ++e) v[e] += q[e];
           }
           const u32x4 pk = Chunk<bf16>::pack(v);
-          *(u32x4*)dst = pk;
+          if (p.wt)
+            __builtin_amdgcn_raw_buffer_store_b128(pk, crs, (int)(((long long)(row - m0) * p.ldc + col) * 2), 0, 16);
+          else
+            *(u32x4*)dst = pk;
           if (smode) Chunk<bf16>::unpack(pk, v);  // statistics of the values as stored
         } else {
           if (cmode == 2) {
@@ -940,8 +945,14 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
 #pragma unroll
             for (int e = 0; e < 4; ++e) { v[e] += q0[e]; v[4 + e] += q1[e]; }
           }
-          *(f32x4*)dst = *(f32x4*)&v[0];
-          *(f32x4*)(dst + 4) = *(f32x4*)&v[4];
+          if (p.wt) {
+            const int off = (int)(((long long)(row - m0) * p.ldc + col) * 4);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *(f32x4*)&v[0]), crs, off, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *(f32x4*)&v[4]), crs, off + 16, 0, 16);
+          } else {
+            *(f32x4*)dst = *(f32x4*)&v[0];
+            *(f32x4*)(dst + 4) = *(f32x4*)&v[4];
+          }
         }
       } else {
 #pragma unroll
@@ -1306,7 +1317,17 @@ static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
   return true;
 }
 
-int cn_gemm_dispatch(const GemmArgs& a, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
+// Write-through C stores (CN_GEMM_WT=1, A/B runs): the C lines go to memory as they are stored
+// instead of sitting dirty in the XCD's L2 until the kernel's end-of-launch write-back.
+static bool wt_on() {
+  static const bool on = [] { const char* e = getenv("CN_GEMM_WT"); return e && e[0] == '1'; }();
+  return on;
+}
+
+int cn_gemm_dispatch(const GemmArgs& a_in, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
+  GemmArgs a = a_in;
+  // per-block 32-bit offsets from the block's first row: not for the stride-2 row scatter
+  a.wt = wt_on() && !a.row_map && a.c_mode != 1;
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
   const int esz = (dtype == DT_FP8 || dtype == DT_FP8_E5M2) ? 1 : dtype == DT_BF16 ? 2 : 4;
   const int bk = 128 / esz;
