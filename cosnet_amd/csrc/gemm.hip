@@ -1317,17 +1317,19 @@ static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
   return true;
 }
 
-// Write-through C stores (CN_GEMM_WT=1, A/B runs): the C lines go to memory as they are stored
-// instead of sitting dirty in the XCD's L2 until the kernel's end-of-launch write-back.
-static bool wt_on() {
-  static const bool on = [] { const char* e = getenv("CN_GEMM_WT"); return e && e[0] == '1'; }();
-  return on;
+// Write-through C stores (A/B runs): the C lines go to memory as they are stored instead of
+// sitting dirty in the XCD's L2 until the kernel's end-of-launch write-back.  CN_GEMM_WT=1: every
+// C store (measured -0.4 % on the step, profiles/r06_write_through_ab.txt); 3: split-K slab stores
+// only (c_mode 3, read back by the reduce kernel).
+static int wt_on() {
+  static const int lvl = [] { const char* e = getenv("CN_GEMM_WT"); return e ? atoi(e) : 0; }();
+  return lvl;
 }
 
 int cn_gemm_dispatch(const GemmArgs& a_in, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   GemmArgs a = a_in;
   // per-block 32-bit offsets from the block's first row: not for the stride-2 row scatter
-  a.wt = wt_on() && !a.row_map && a.c_mode != 1;
+  a.wt = !a.row_map && a.c_mode != 1 && (wt_on() == 1 || (wt_on() == 3 && a.c_mode == 3));
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
   const int esz = (dtype == DT_FP8 || dtype == DT_FP8_E5M2) ? 1 : dtype == DT_BF16 ? 2 : 4;
   const int bk = 128 / esz;
