@@ -56,7 +56,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
 // in the XCD's L2 for the end-of-kernel write-back that the next kernel's start waits on
 // (+0.55 % on the step; the same for the GEMM epilogue's C stores measured -0.4 %:
 // profiles/r06_write_through_ab.txt).  CN_BN_WT=0: plain stores; 2: also the ReLU-mask bytes and
-// the fp8 output copy (A/B runs).
+// the fp8 output copy; 3: non-temporal (nt) stores instead (A/B runs).
 static int bn_wt_env() {
   static const int lvl = [] { const char* e = getenv("CN_BN_WT"); return e ? atoi(e) : 1; }();
   return lvl;
@@ -429,7 +429,9 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         f[u][v] = t;
       }
       const u32x4 pk = Chunk<T>::pack(f[u]);
-      if (wt)
+      if (wt == 3)
+        __builtin_nontemporal_store(pk, (u32x4*)(y + r * ldy + c0));
+      else if (wt)
         __builtin_amdgcn_raw_buffer_store_b128(pk, yrs, (int)((r * ldy + c0) * (long long)sizeof(T)), 0, 16);
       else
         *(u32x4*)(y + r * ldy + c0) = pk;
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
         unsigned bits = 0;
 #pragma unroll
         for (int v = 0; v < V; ++v) bits |= (sv[v] > 0.f ? 1u : 0u) << v;
-        if (wt > 1)
+        if (wt == 2)
           __builtin_amdgcn_raw_buffer_store_b8((unsigned char)bits, mkrs, (int)(r * ldm + chunk), 0, 16);
         else
           mk[r * ldm + chunk] = (unsigned char)bits;
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(256) void bn_apply_k(const T* __restrict__ x, long 
           u32x2 o;
           o.x = pack4_fp8_bn(f[u][v] * qinv, f[u][v + 1] * qinv, f[u][v + 2] * qinv, f[u][v + 3] * qinv);
           o.y = pack4_fp8_bn(f[u][v + 4] * qinv, f[u][v + 5] * qinv, f[u][v + 6] * qinv, f[u][v + 7] * qinv);
-          if (wt > 1)
+          if (wt == 2)
             __builtin_amdgcn_raw_buffer_store_b64(o, y8rs, (int)(r * ldy8 + c0 + v), 0, 16);
           else
             *(u32x2*)(y8 + r * ldy8 + c0 + v) = o;
@@ -644,7 +646,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const T* __restrict__ x, l
         o[v] = k1[v] * (dd - m1[v] - xh * m2[v]);
         d[u][v] = dd;
       }
-      if (wt) {
+      if (wt == 3) {
+        __builtin_nontemporal_store(Chunk<T>::pack(o), (u32x4*)(dx + (long long)r * lddx + chunk * V));
+        if (dres) __builtin_nontemporal_store(Chunk<T>::pack(d[u]), (u32x4*)(dres + (long long)r * lddres + chunk * V));
+      } else if (wt) {
         st_chunk_wt<T>(dxr, ((long long)r * lddx + chunk * V) * (long long)sizeof(T), o);
         if (dres) st_chunk_wt<T>(drr, ((long long)r * lddres + chunk * V) * (long long)sizeof(T), d[u]);
       } else {
@@ -843,7 +848,7 @@ extern "C" int cn_bn_apply_ex(int dtype, const void* x, long long ldx, int P, in
     return CN_ERR_ALIGN;
   if (P < 1 || nseg < 1) return CN_ERR_SHAPE;
   int wt = bn_wt((long long)nseg * P, ldy, dtype == DT_BF16 ? 2 : 4);
-  if (wt > 1 && ((mask && !bn_wt((long long)nseg * P, ldm, 1)) || (y8 && !bn_wt((long long)nseg * P, ldy8, 1))))
+  if (wt == 2 && ((mask && !bn_wt((long long)nseg * P, ldm, 1)) || (y8 && !bn_wt((long long)nseg * P, ldy8, 1))))
     wt = 1;
   int gx, gy;
   if (dtype == DT_BF16) {

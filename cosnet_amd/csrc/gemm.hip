@@ -934,7 +934,9 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
             for (int e = 0; e < 8; ++e) v[e] += q[e];
           }
           const u32x4 pk = Chunk<bf16>::pack(v);
-          if (p.wt)
+          if (p.wt == 4)
+            __builtin_nontemporal_store(pk, (u32x4*)dst);
+          else if (p.wt)
             __builtin_amdgcn_raw_buffer_store_b128(pk, crs, (int)(((long long)(row - m0) * p.ldc + col) * 2), 0, 16);
           else
             *(u32x4*)dst = pk;
@@ -945,7 +947,10 @@ __global__ __launch_bounds__(WM * WN * 64 * (PP == 2 ? 2 : 1), (EPI && sizeof(T)
 #pragma unroll
             for (int e = 0; e < 4; ++e) { v[e] += q0[e]; v[4 + e] += q1[e]; }
           }
-          if (p.wt) {
+          if (p.wt == 4) {
+            __builtin_nontemporal_store(*(f32x4*)&v[0], (f32x4*)dst);
+            __builtin_nontemporal_store(*(f32x4*)&v[4], (f32x4*)(dst + 4));
+          } else if (p.wt) {
             const int off = (int)(((long long)(row - m0) * p.ldc + col) * 4);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *(f32x4*)&v[0]), crs, off, 0, 16);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, *(f32x4*)&v[4]), crs, off + 16, 0, 16);
@@ -1320,7 +1325,8 @@ static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
 // Write-through C stores (A/B runs): the C lines go to memory as they are stored instead of
 // sitting dirty in the XCD's L2 until the kernel's end-of-launch write-back.  CN_GEMM_WT=1: every
 // C store (measured -0.4 % on the step, profiles/r06_write_through_ab.txt); 3: split-K slab stores
-// only (c_mode 3, read back by the reduce kernel).
+// only (c_mode 3, read back by the reduce kernel; -1.4 %); 4: non-temporal (nt) stores of C (not the
+// slabs) instead.
 static int wt_on() {
   static const int lvl = [] { const char* e = getenv("CN_GEMM_WT"); return e ? atoi(e) : 0; }();
   return lvl;
@@ -1329,7 +1335,8 @@ static int wt_on() {
 int cn_gemm_dispatch(const GemmArgs& a_in, int dtype, int c_f32, int la, int lb, int batch, hipStream_t st) {
   GemmArgs a = a_in;
   // per-block 32-bit offsets from the block's first row: not for the stride-2 row scatter
-  a.wt = !a.row_map && a.c_mode != 1 && (wt_on() == 1 || (wt_on() == 3 && a.c_mode == 3));
+  a.wt = wt_on() == 4 ? (a.c_mode != 1 && a.c_mode != 3 ? 4 : 0)
+                      : !a.row_map && a.c_mode != 1 && (wt_on() == 1 || (wt_on() == 3 && a.c_mode == 3));
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
   const int esz = (dtype == DT_FP8 || dtype == DT_FP8_E5M2) ? 1 : dtype == DT_BF16 ? 2 : 4;
   const int bk = 128 / esz;
