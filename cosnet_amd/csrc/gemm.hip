@@ -1322,13 +1322,13 @@ static bool buf_ok(int kind, const GemmArgs& a, bool is_a, int esz) {
   return true;
 }
 
-// Write-through C stores (A/B runs): the C lines go to memory as they are stored instead of
-// sitting dirty in the XCD's L2 until the kernel's end-of-launch write-back.  CN_GEMM_WT=1: every
-// C store (measured -0.4 % on the step, profiles/r06_write_through_ab.txt); 3: split-K slab stores
-// only (c_mode 3, read back by the reduce kernel; -1.4 %); 4: non-temporal (nt) stores of C (not the
-// slabs) instead.
+// C store policy.  Default (CN_GEMM_WT=4): non-temporal (nt) stores of C -- the split-K slabs,
+// which the reduce kernel reads back, excepted -- +0.5 % on the step (profiles/r06_write_through_ab.txt:
+// the lines leave the L2 early instead of waiting dirty for the end-of-launch write-back).  A/B
+// variants: 0 plain stores; 1 write-through (sc1) for every C store (-0.4 %); 3 write-through for the
+// split-K slabs only (-1.4 %).
 static int wt_on() {
-  static const int lvl = [] { const char* e = getenv("CN_GEMM_WT"); return e ? atoi(e) : 0; }();
+  static const int lvl = [] { const char* e = getenv("CN_GEMM_WT"); return e ? atoi(e) : 4; }();
   return lvl;
 }
 
